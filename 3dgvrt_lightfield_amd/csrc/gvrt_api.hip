@@ -1,0 +1,392 @@
+// gvrt_api.hip — the C-ABI of include/gvrt.h: handle lifetime, device memory, launches.
+//
+// The library owns all device memory (splats, proxies, LBVH, scratch); callers own host
+// arrays (copied during the call) and output surfaces.  No pointer is retained after a call.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "gvrt_internal.h"
+
+using namespace gvrt;
+
+static thread_local std::string g_global_err;
+
+gvrt_status gvrt_fail(gvrt_context* c, gvrt_status code, const std::string& msg) {
+    if (c) c->err = msg;
+    else g_global_err = msg;
+    return code;
+}
+
+gvrt_status gvrt_hip_check(gvrt_context* c, hipError_t e, const char* what) {
+    if (e == hipSuccess) return GVRT_OK;
+    std::string m = std::string(what) + ": " + hipGetErrorString(e);
+    return gvrt_fail(c, e == hipErrorOutOfMemory ? GVRT_ERR_OOM : GVRT_ERR_HIP, m);
+}
+
+gvrt_status gvrt_dalloc(gvrt_context* c, void** p, uint64_t bytes) {
+    *p = nullptr;
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) {
+        *p = nullptr;
+        (void)hipGetLastError();
+        return gvrt_hip_check(c, e, "hipMalloc");
+    }
+    c->allocs[*p] = bytes;
+    c->device_bytes += bytes;
+    return GVRT_OK;
+}
+
+void gvrt_dfree(gvrt_context* c, void** p) {
+    if (!*p) return;
+    auto it = c->allocs.find(*p);
+    if (it != c->allocs.end()) {
+        c->device_bytes -= it->second;
+        c->allocs.erase(it);
+    }
+    (void)hipFree(*p);
+    *p = nullptr;
+}
+
+extern "C" {
+
+int gvrt_abi_version(void) { return GVRT_ABI_VERSION; }
+
+const char* gvrt_build_info(void) {
+    return "gvrt " "abi1 gfx950 hip" " (" __DATE__ " " __TIME__ ")";
+}
+
+void gvrt_default_enclosing_params(gvrt_enclosing_params* p) {
+    if (!p) return;
+    p->kernel_min_response = 0.0113f;  // VulkanFullRT.cpp:1354
+    p->opts = 0;                       // MOGRenderNone, VulkanFullRT.cpp:1355
+    p->degree = 4.0f;                  // VulkanFullRT.cpp:1356
+    p->emit_triangles = 0;
+}
+
+void gvrt_default_render_params(gvrt_render_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    const float aabb[6] = {-100.f, -100.f, -100.f, 100.f, 100.f, 100.f};  // VulkanUtils.h:53
+    std::memcpy(p->aabb, aabb, sizeof(aabb));
+    p->min_transmittance = 0.001f;          // VulkanUtils.h:54
+    p->hit_min_gaussian_response = 0.0113f;  // VulkanUtils.h:55
+    p->sph_eval_degree = 3;                  // VulkanUtils.h:56
+    p->alpha_min = 0.0039215686275f;         // 3dgs.glsl:16
+    p->pixel_offset = 0.0f;                  // RQ variant (particleRendering.comp:124)
+    p->alpha_init = 0.0f;                    // RQ variant (particleRendering.comp:132)
+    p->tmin_inclusive = 0;
+    p->mode = GVRT_MODE_FAST;
+    p->max_rounds = 0;
+    p->ray_dirs_layout = 0;
+}
+
+gvrt_status gvrt_device_count(int* count) {
+    if (!count) return gvrt_fail(nullptr, GVRT_ERR_INVALID_ARG, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        *count = 0;
+        return GVRT_OK;
+    }
+    *count = n;
+    return GVRT_OK;
+}
+
+gvrt_status gvrt_create(int device, gvrt_handle* out) {
+    if (!out) return gvrt_fail(nullptr, GVRT_ERR_INVALID_ARG, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) {
+        (void)hipGetLastError();
+        return gvrt_fail(nullptr, GVRT_ERR_NO_DEVICE, "no HIP device available");
+    }
+    if (device < 0 || device >= n) return gvrt_fail(nullptr, GVRT_ERR_INVALID_ARG, "device index out of range");
+    gvrt_context* c = new (std::nothrow) gvrt_context();
+    if (!c) return gvrt_fail(nullptr, GVRT_ERR_OOM, "host allocation failed");
+    c->device = device;
+    e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e != hipSuccess) {
+        gvrt_status s = gvrt_hip_check(nullptr, e, "gvrt_create");
+        delete c;
+        return s;
+    }
+    if (gvrt_dalloc(c, (void**)&c->d_stats, 64) != GVRT_OK) {
+        delete c;
+        return gvrt_fail(nullptr, GVRT_ERR_OOM, "stats alloc");
+    }
+    *out = c;
+    return GVRT_OK;
+}
+
+gvrt_status gvrt_destroy(gvrt_handle c) {
+    if (!c) return GVRT_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    std::vector<void*> ptrs;
+    for (auto& kv : c->allocs) ptrs.push_back(kv.first);
+    for (void* p : ptrs) (void)hipFree(p);
+    c->allocs.clear();
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return GVRT_OK;
+}
+
+const char* gvrt_last_error(gvrt_handle c) { return c ? c->err.c_str() : g_global_err.c_str(); }
+
+gvrt_status gvrt_load_splats(gvrt_handle c, const gvrt_splats* s) {
+    if (!c || !s) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL argument");
+    if (s->n && (!s->positions || !s->f_dc || !s->f_rest || !s->opacity || !s->scale || !s->rotation))
+        return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL splat array");
+    if (s->n > 0xFFFFFFFFull) return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "more than 2^32-1 splats");
+    GVRT_HIP(c, hipSetDevice(c->device));
+    gvrt_dfree(c, (void**)&c->d_pos);
+    gvrt_dfree(c, (void**)&c->d_rot);
+    gvrt_dfree(c, (void**)&c->d_scl);
+    gvrt_dfree(c, (void**)&c->d_opa);
+    gvrt_dfree(c, (void**)&c->d_fdc);
+    gvrt_dfree(c, (void**)&c->d_frest);
+    c->enclosed = false;
+    c->accel = false;
+    c->m = 0;
+    const uint64_t n = s->n;
+    gvrt_status st;
+    if ((st = gvrt_dalloc(c, (void**)&c->d_pos, 12 * n))) return st;
+    if ((st = gvrt_dalloc(c, (void**)&c->d_rot, 16 * n))) return st;
+    if ((st = gvrt_dalloc(c, (void**)&c->d_scl, 12 * n))) return st;
+    if ((st = gvrt_dalloc(c, (void**)&c->d_opa, 4 * n))) return st;
+    if ((st = gvrt_dalloc(c, (void**)&c->d_fdc, 12 * n))) return st;
+    if ((st = gvrt_dalloc(c, (void**)&c->d_frest, 180 * n + 360))) return st;
+    if (n) {
+        GVRT_HIP(c, hipMemcpyAsync(c->d_pos, s->positions, 12 * n, hipMemcpyHostToDevice, c->stream));
+        GVRT_HIP(c, hipMemcpyAsync(c->d_rot, s->rotation, 16 * n, hipMemcpyHostToDevice, c->stream));
+        GVRT_HIP(c, hipMemcpyAsync(c->d_scl, s->scale, 12 * n, hipMemcpyHostToDevice, c->stream));
+        GVRT_HIP(c, hipMemcpyAsync(c->d_opa, s->opacity, 4 * n, hipMemcpyHostToDevice, c->stream));
+        GVRT_HIP(c, hipMemcpyAsync(c->d_fdc, s->f_dc, 12 * n, hipMemcpyHostToDevice, c->stream));
+        GVRT_HIP(c, hipMemcpyAsync(c->d_frest, s->f_rest, 180 * n, hipMemcpyHostToDevice, c->stream));
+    }
+    GVRT_HIP(c, hipMemsetAsync(reinterpret_cast<char*>(c->d_frest) + 180 * n, 0, 360, c->stream));
+    GVRT_HIP(c, hipStreamSynchronize(c->stream));
+    c->n = n;
+    c->stats.n_input = n;
+    return GVRT_OK;
+}
+
+gvrt_status gvrt_build_enclosing(gvrt_handle c, const gvrt_enclosing_params* p, uint64_t* m) {
+    if (!c) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL handle");
+    gvrt_enclosing_params def;
+    gvrt_default_enclosing_params(&def);
+    if (!p) p = &def;
+    if (!c->d_pos) return gvrt_fail(c, GVRT_ERR_STATE, "gvrt_load_splats has not been called");
+    GVRT_HIP(c, hipSetDevice(c->device));
+    uint64_t mm = 0;
+    gvrt_status s = gvrt_launch_enclose(c, p, &mm);
+    if (s) return s;
+    c->enc = *p;
+    c->m = mm;
+    c->enclosed = true;
+    c->accel = false;
+    c->stats.n_survivors = mm;
+    if (m) *m = mm;
+    return GVRT_OK;
+}
+
+gvrt_status gvrt_read_enclosing(gvrt_handle c, float* density12, float* sh48, float* verts36, uint32_t* tris60,
+                                uint32_t* src_index) {
+    if (!c) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL handle");
+    if (!c->enclosed) return gvrt_fail(c, GVRT_ERR_STATE, "enclosing pass has not run");
+    GVRT_HIP(c, hipSetDevice(c->device));
+    const uint64_t m = c->m;
+    if ((verts36 || tris60) && !c->enc.emit_triangles)
+        return gvrt_fail(c, GVRT_ERR_STATE, "triangles requested but emit_triangles was 0");
+    if (m) {
+        if (density12) GVRT_HIP(c, hipMemcpyAsync(density12, c->d_density12, 48 * m, hipMemcpyDeviceToHost, c->stream));
+        if (sh48) GVRT_HIP(c, hipMemcpyAsync(sh48, c->d_sh48, 192 * m, hipMemcpyDeviceToHost, c->stream));
+        if (verts36) GVRT_HIP(c, hipMemcpyAsync(verts36, c->d_verts, 144 * m, hipMemcpyDeviceToHost, c->stream));
+        if (tris60) GVRT_HIP(c, hipMemcpyAsync(tris60, c->d_tris, 240 * m, hipMemcpyDeviceToHost, c->stream));
+        if (src_index) GVRT_HIP(c, hipMemcpyAsync(src_index, c->d_src, 4 * m, hipMemcpyDeviceToHost, c->stream));
+    }
+    GVRT_HIP(c, hipStreamSynchronize(c->stream));
+    return GVRT_OK;
+}
+
+gvrt_status gvrt_build_accel(gvrt_handle c) {
+    if (!c) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL handle");
+    if (!c->enclosed) return gvrt_fail(c, GVRT_ERR_STATE, "gvrt_build_enclosing has not been called");
+    GVRT_HIP(c, hipSetDevice(c->device));
+    return gvrt_launch_build_accel(c);
+}
+
+gvrt_status gvrt_set_stats(gvrt_handle c, int enable) {
+    if (!c) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL handle");
+    c->stats_on = enable != 0;
+    return GVRT_OK;
+}
+
+gvrt_status gvrt_get_stats(gvrt_handle c, gvrt_stats* s) {
+    if (!c || !s) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL argument");
+    c->stats.device_bytes = c->device_bytes;
+    *s = c->stats;
+    return GVRT_OK;
+}
+
+static gvrt_status ensure(gvrt_context* c, void** p, uint64_t* cap, uint64_t bytes) {
+    if (*cap >= bytes && *p) return GVRT_OK;
+    gvrt_dfree(c, p);
+    *cap = 0;
+    gvrt_status s = gvrt_dalloc(c, p, bytes);
+    if (s) return s;
+    *cap = bytes;
+    return GVRT_OK;
+}
+
+gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float* view_inverse,
+                        const float* proj_inverse, uint32_t width, uint32_t height, uint32_t ncams,
+                        const gvrt_tile* tiles, uint64_t ntiles, const gvrt_image* out) {
+    if (!c) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL handle");
+    if (!view_inverse || !proj_inverse || !out) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL argument");
+    if (width == 0 || height == 0 || ncams == 0) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "empty image");
+    if (width > 32768 || height > 32768 || ncams > 255)
+        return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "image larger than 32768^2 or more than 255 cameras");
+    if (!c->accel) return gvrt_fail(c, GVRT_ERR_STATE, "gvrt_build_accel has not been called");
+    gvrt_render_params def;
+    gvrt_default_render_params(&def);
+    if (!p) p = &def;
+    if (p->mode > GVRT_MODE_LITERAL) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "unknown mode");
+    if (p->tmin_inclusive && (p->mode != GVRT_MODE_LITERAL || p->max_rounds == 0))
+        return gvrt_fail(c, GVRT_ERR_INVALID_ARG,
+                         "tmin_inclusive needs mode LITERAL and max_rounds > 0 (an inclusive tmin re-finds the last "
+                         "hit every round and never terminates when it is rejected)");
+    if (out->packed && !tiles) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "packed output needs a tile list");
+    if (out->packed && out->ray_dirs) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "ray_dirs cannot be packed");
+    GVRT_HIP(c, hipSetDevice(c->device));
+
+    const uint32_t tiles_x = (width + 7) / 8, tiles_y = (height + 7) / 8;
+    const uint64_t total_tiles = (uint64_t)tiles_x * tiles_y * ncams;
+    gvrt_status s;
+    RenderArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.recs = c->d_recs;
+    a.sh = c->d_sh;
+    a.nodes = c->d_nodes;
+    a.nrecs = (uint32_t)c->m;
+    a.root_is_leaf = c->m == 1 ? 1u : 0u;
+    // cameras
+    if ((s = ensure(c, (void**)&c->d_viewinv, &c->viewinv_cap, 64ull * ncams))) return s;
+    GVRT_HIP(c, hipMemcpyAsync(c->d_viewinv, view_inverse, 64ull * ncams, hipMemcpyHostToDevice, c->stream));
+    a.view_inv = c->d_viewinv;
+    std::memcpy(a.proj_inv, proj_inverse, 64);
+    std::memcpy(a.aabb, p->aabb, 24);
+    a.min_transmittance = p->min_transmittance;
+    a.min_response = p->hit_min_gaussian_response;
+    a.alpha_min = p->alpha_min;
+    a.pixel_offset = p->pixel_offset;
+    a.alpha_init = p->alpha_init;
+    a.kmin = c->enc.kernel_min_response;
+    a.kdeg = c->enc.degree;
+    a.kopts = c->enc.opts;
+    a.kernel_h = kernel_scale(1.0f, a.kmin, a.kopts & ~1u, a.kdeg) * SQRT3;
+    a.sph_deg = p->sph_eval_degree;
+    a.width = width;
+    a.height = height;
+    a.ncams = ncams;
+    a.tiles_x = tiles_x;
+    a.tiles_y = tiles_y;
+    a.tmin_inclusive = p->tmin_inclusive;
+    a.max_rounds = p->max_rounds;
+    a.ray_dirs_layout = p->ray_dirs_layout;
+    a.packed = out->packed;
+    uint64_t nwork = total_tiles;
+    if (tiles) {
+        std::vector<uint32_t> tl(ntiles);
+        for (uint64_t i = 0; i < ntiles; ++i) {
+            if (tiles[i].tx >= tiles_x || tiles[i].ty >= tiles_y || tiles[i].cam >= ncams)
+                return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "tile outside the image");
+            tl[i] = ((uint32_t)tiles[i].cam << 24) | ((uint32_t)tiles[i].ty << 12) | tiles[i].tx;
+        }
+        if ((s = ensure(c, (void**)&c->d_tiles, &c->tiles_cap, 4 * (ntiles ? ntiles : 1)))) return s;
+        if (ntiles) GVRT_HIP(c, hipMemcpyAsync(c->d_tiles, tl.data(), 4 * ntiles, hipMemcpyHostToDevice, c->stream));
+        a.tiles = c->d_tiles;
+        nwork = ntiles;
+    }
+    a.ntiles = nwork;
+    const uint64_t npix = out->packed ? nwork * 64 : (uint64_t)width * height * ncams;
+
+    // outputs: device pointers used directly; host pointers staged
+    const uint64_t b8 = out->rgba8 ? 4 * npix : 0;
+    const uint64_t b32 = out->rgba32f ? 16 * npix : 0;
+    const uint64_t bdir = out->ray_dirs ? 16ull * width * height * ncams : 0;
+    const uint64_t bhc = out->hit_counts ? 4 * npix : 0;
+    if (out->device_ptrs) {
+        a.rgba8 = (uint8_t*)out->rgba8;
+        a.rgba32f = out->rgba32f;
+        a.ray_dirs = out->ray_dirs;
+        a.hit_counts = out->hit_counts;
+    } else {
+        const uint64_t total = b8 + b32 + bdir + bhc;
+        if ((s = ensure(c, &c->d_stage, &c->stage_cap, total ? total : 16))) return s;
+        char* base = (char*)c->d_stage;
+        uint64_t off = 0;
+        if (b32) { a.rgba32f = (float*)(base + off); off += b32; }
+        if (bdir) { a.ray_dirs = (float*)(base + off); off += bdir; }
+        if (bhc) { a.hit_counts = (uint32_t*)(base + off); off += bhc; }
+        if (b8) { a.rgba8 = (uint8_t*)(base + off); off += b8; }
+        if (!out->packed && tiles) {
+            // pixels outside the tile list keep zeros
+            GVRT_HIP(c, hipMemsetAsync(base, 0, total, c->stream));
+        }
+    }
+    if (c->stats_on) {
+        GVRT_HIP(c, hipMemsetAsync(c->d_stats, 0, 24, c->stream));
+        a.stats = c->d_stats;
+    }
+    GVRT_HIP(c, hipEventRecord(c->ev0, c->stream));
+    if ((s = gvrt_launch_render_mode(c, a, nwork, p->mode == GVRT_MODE_LITERAL))) return s;
+    GVRT_HIP(c, hipEventRecord(c->ev1, c->stream));
+    if (!out->device_ptrs) {
+        if (b32) GVRT_HIP(c, hipMemcpyAsync(out->rgba32f, a.rgba32f, b32, hipMemcpyDeviceToHost, c->stream));
+        if (bdir) GVRT_HIP(c, hipMemcpyAsync(out->ray_dirs, a.ray_dirs, bdir, hipMemcpyDeviceToHost, c->stream));
+        if (bhc) GVRT_HIP(c, hipMemcpyAsync(out->hit_counts, a.hit_counts, bhc, hipMemcpyDeviceToHost, c->stream));
+        if (b8) GVRT_HIP(c, hipMemcpyAsync(out->rgba8, a.rgba8, b8, hipMemcpyDeviceToHost, c->stream));
+    }
+    unsigned long long hs[3] = {0, 0, 0};
+    if (c->stats_on) GVRT_HIP(c, hipMemcpyAsync(hs, c->d_stats, 24, hipMemcpyDeviceToHost, c->stream));
+    GVRT_HIP(c, hipStreamSynchronize(c->stream));
+    float ms = 0.f;
+    GVRT_HIP(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->stats.render_ms = ms;
+    c->stats.rays = nwork * 64;
+    c->stats.crossings = hs[0];
+    c->stats.accepted = hs[1];
+    c->stats.rounds = hs[2];
+    return GVRT_OK;
+}
+
+gvrt_status gvrt_unpack_tiles_rgba8(gvrt_handle c, const void* packed, const gvrt_tile* tiles, uint64_t ntiles,
+                                    uint32_t width, uint32_t height, void* frame) {
+    if (!c || !packed || !tiles || !frame) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL argument");
+    GVRT_HIP(c, hipSetDevice(c->device));
+    std::vector<uint32_t> tl(ntiles);
+    for (uint64_t i = 0; i < ntiles; ++i)
+        tl[i] = ((uint32_t)tiles[i].cam << 24) | ((uint32_t)tiles[i].ty << 12) | tiles[i].tx;
+    gvrt_status s;
+    if ((s = ensure(c, (void**)&c->d_tiles, &c->tiles_cap, 4 * (ntiles ? ntiles : 1)))) return s;
+    if (ntiles) GVRT_HIP(c, hipMemcpyAsync(c->d_tiles, tl.data(), 4 * ntiles, hipMemcpyHostToDevice, c->stream));
+    if ((s = gvrt_launch_unpack(c, packed, c->d_tiles, ntiles, width, height, frame))) return s;
+    GVRT_HIP(c, hipStreamSynchronize(c->stream));
+    return GVRT_OK;
+}
+
+}  // extern "C"

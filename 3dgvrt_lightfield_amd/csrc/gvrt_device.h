@@ -1,0 +1,108 @@
+// gvrt_device.h — device-side records and math shared by the gfx950 kernels.
+//
+// HBM layout (per survivor, BVH-leaf order after gvrt_build_accel):
+//   RenderRec  64 B   everything processHit needs except SH: position, activated density,
+//                     R = quaternionWXYZToMatrix(q) (utils.glsl:13-34, i.e. R^T of the
+//                     world rotation) as three GLSL columns, 1/scale.  One s_load_dwordx16.
+//   SH         192 B  [f_dc.rgb, f_rest 45] (particlePrimitives.comp:207-214), read only for
+//                     accepted crossings (fetchParticleSphCoefficients, gaussianfunctions.glsl:104-115)
+//   BvhNode    64 B   two child AABBs inline + child links (LBVH, Karras 2012)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gvrt {
+
+constexpr float EPS_T = 1e-9f;                        // 3dgs.glsl:13
+constexpr int K_HITS = 16;                            // MAX_HIT_PER_TRACE, 3dgs.glsl:15
+constexpr uint32_t INVALID_ID = 0xFFFFFFFFu;          // 3dgs.glsl:26
+constexpr float INF_DIST = 1e20f;                     // 3dgs.glsl:27
+constexpr float KERNEL_S = -0.0555555555556f;         // degree-4 response, gaussianfunctions.glsl:31-35
+constexpr float PHI = 1.618033988749895f;             // particlePrimitives.comp:77
+constexpr float IPHI = 0.618033988749895f;
+constexpr float ICOSA_VRT_SCALE = 0.5f * 1.323169076499215f;  // particlePrimitives.comp:78-79
+constexpr float SQRT3 = 1.7320508075688772f;
+constexpr int STACK_DEPTH = 128;                      // per-wave LDS traversal stack
+
+struct alignas(16) RenderRec {
+    float px, py, pz, density;
+    float c0x, c0y, c0z, c1x;  // GLSL mat3 columns of quaternionWXYZToMatrix(q)
+    float c1y, c1z, c2x, c2y;
+    float c2z, isx, isy, isz;  // giscl = 1/scale
+};
+static_assert(sizeof(RenderRec) == 64, "RenderRec must be 64 B");
+
+struct alignas(16) BvhNode {
+    float l0x, l0y, l0z, h0x;
+    float h0y, h0z, l1x, l1y;
+    float l1z, h1x, h1y, h1z;
+    int32_t c0, c1;  // >= 0 internal node index; < 0 leaf ~index (record index)
+    uint32_t pad0, pad1;
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 B");
+
+struct f3 {
+    float x, y, z;
+};
+__host__ __device__ inline f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
+__host__ __device__ inline f3 operator+(f3 a, f3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__host__ __device__ inline f3 operator-(f3 a, f3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__host__ __device__ inline f3 operator*(f3 a, f3 b) { return mk3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__host__ __device__ inline f3 operator*(f3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
+__host__ __device__ inline float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__host__ __device__ inline f3 cross3(f3 a, f3 b) {
+    return mk3(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
+}
+
+// Render-kernel launch arguments (one struct, passed by value).
+struct RenderArgs {
+    const RenderRec* __restrict__ recs;
+    const float* __restrict__ sh;        // 48 f32 per record
+    const BvhNode* __restrict__ nodes;
+    const float* __restrict__ view_inv;  // 16 per camera, column-major
+    const uint32_t* __restrict__ tiles;  // packed (cam<<24 | ty<<12 | tx) or null
+    float proj_inv[16];
+    float aabb[6];
+    float min_transmittance;
+    float min_response;
+    float alpha_min;
+    float pixel_offset;
+    float alpha_init;
+    float kernel_h;      // sqrt(3) * kernelScale (uniform when opts has no adaptive clamping)
+    float kmin;          // enclosing kernelMinResponse (adaptive clamping recomputes kS per particle)
+    float kdeg;
+    uint32_t kopts;
+    uint32_t sph_deg;
+    uint32_t width, height, ncams;
+    uint32_t tiles_x, tiles_y;
+    uint64_t ntiles;
+    uint32_t nrecs;
+    uint32_t tmin_inclusive;
+    uint32_t max_rounds;
+    uint32_t ray_dirs_layout;
+    uint32_t packed;
+    uint32_t root_is_leaf;   // M == 1
+    uint8_t* rgba8;
+    float* rgba32f;
+    float* ray_dirs;
+    uint32_t* hit_counts;
+    unsigned long long* stats;  // [crossings, accepted, rounds] or null
+};
+
+// kernelScale, particlePrimitives.comp:81-105
+__host__ __device__ inline float kernel_scale(float density, float modulatedMinResponse, uint32_t opts,
+                                              float kernelDegree) {
+    const float responseModulation = (opts & 1u) != 0 ? density : 1.0f;
+    const float minResponse = fminf(modulatedMinResponse / responseModulation, 0.97f);
+    if (kernelDegree < 0) {
+        const float k = fabsf(kernelDegree);
+        const float s = 1.0f / powf(3.0f, k);
+        return powf((1.f / (logf(minResponse) - 1.f) + 1.f) / s, 1.f / k);
+    }
+    if (kernelDegree == 0) return ((1.0f - minResponse) / 3.0f) / -0.329630334487f;
+    const float b = kernelDegree;
+    const float a = -4.5f / powf(3.0f, b);
+    return powf(logf(minResponse) / a, 1.0f / b);
+}
+
+}  // namespace gvrt

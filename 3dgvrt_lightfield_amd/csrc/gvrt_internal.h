@@ -1,0 +1,82 @@
+// gvrt_internal.h — the handle behind gvrt.h and the launchers each .hip file provides.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <unordered_map>
+
+#include "../../include/gvrt.h"
+#include "gvrt_device.h"
+
+struct gvrt_context {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+    uint64_t device_bytes = 0;
+    std::unordered_map<void*, uint64_t> allocs;
+
+    // splat inputs (Model::allocateAttributeBuffers, Vulkan3DGRTModel.cpp:163-222)
+    uint64_t n = 0;
+    float* d_pos = nullptr;    // 3n
+    float* d_rot = nullptr;    // 4n
+    float* d_scl = nullptr;    // 3n
+    float* d_opa = nullptr;    // n
+    float* d_fdc = nullptr;    // 3n
+    float* d_frest = nullptr;  // 45n + 90 zero pad (Q5 out-of-bounds reads read 0)
+
+    // enclosing outputs, compaction order (saveIdx)
+    bool enclosed = false;
+    gvrt_enclosing_params enc{};
+    uint64_t m = 0;
+    uint64_t cap = 0;
+    float* d_density12 = nullptr;
+    float* d_sh48 = nullptr;
+    float* d_verts = nullptr;
+    uint32_t* d_tris = nullptr;
+    uint32_t* d_src = nullptr;
+    gvrt::RenderRec* d_recs_c = nullptr;
+    float* d_boxes_c = nullptr;  // 6 per survivor
+    uint32_t* d_flags = nullptr;
+    uint32_t* d_scan = nullptr;
+
+    // acceleration structure, leaf order
+    bool accel = false;
+    gvrt::RenderRec* d_recs = nullptr;
+    float* d_sh = nullptr;
+    gvrt::BvhNode* d_nodes = nullptr;
+    uint32_t* d_leaf_src = nullptr;  // leaf -> compaction index
+    uint32_t depth = 0;
+
+    // per-render scratch
+    bool stats_on = false;
+    unsigned long long* d_stats = nullptr;
+    uint32_t* d_tiles = nullptr;
+    uint64_t tiles_cap = 0;
+    float* d_viewinv = nullptr;
+    uint64_t viewinv_cap = 0;
+    void* d_stage = nullptr;  // staging for host outputs
+    uint64_t stage_cap = 0;
+
+    gvrt_stats stats{};
+};
+
+gvrt_status gvrt_fail(gvrt_context* c, gvrt_status code, const std::string& msg);
+gvrt_status gvrt_hip_check(gvrt_context* c, hipError_t e, const char* what);
+gvrt_status gvrt_dalloc(gvrt_context* c, void** p, uint64_t bytes);
+void gvrt_dfree(gvrt_context* c, void** p);
+
+#define GVRT_HIP(ctx, expr)                                         \
+    do {                                                            \
+        hipError_t _e = (expr);                                     \
+        if (_e != hipSuccess) return gvrt_hip_check(ctx, _e, #expr); \
+    } while (0)
+
+// gvrt_enclose.hip
+gvrt_status gvrt_launch_enclose(gvrt_context* c, const gvrt_enclosing_params* p, uint64_t* m);
+// gvrt_lbvh.hip
+gvrt_status gvrt_launch_build_accel(gvrt_context* c);
+// gvrt_render.hip
+gvrt_status gvrt_launch_render_mode(gvrt_context* c, const gvrt::RenderArgs& a, uint64_t nwaves, bool literal);
+gvrt_status gvrt_launch_unpack(gvrt_context* c, const void* packed, const uint32_t* tiles,
+                               uint64_t ntiles, uint32_t width, uint32_t height, void* frame);

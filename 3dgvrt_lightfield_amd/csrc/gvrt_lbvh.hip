@@ -1,0 +1,335 @@
+// gvrt_lbvh.hip — linear BVH over the enclosing proxies, built on gfx950.
+//
+// Replaces the driver BLAS/TLAS builds of VulkanFullRT::createBottomLevelAccelerationStructure3DGRT
+// and createTopLevelAccelerationStructure3DGRT (VulkanFullRT.cpp:575-787).  The reference builds
+// a BLAS over the 20 triangles of every proxy (20N primitives, Q4); here one leaf is one proxy
+// (the render kernel clips the ray against the analytic icosahedron), so the tree has M leaves.
+//
+//   1. centroid bounds        (block reduction + ordered-uint atomics)
+//   2. 30-bit Morton codes    (10 bits per axis)
+//   3. stable radix sort      (rocPRIM via hipcub, keys 30 bits, values = compaction index)
+//   4. permute records        (render records, SH, boxes into leaf order: leaf j = record j)
+//   5. Karras 2012 hierarchy  (one thread per internal node; index tie-break for equal codes)
+//   6. bottom-up AABB refit   (one thread per leaf; agent-scope acq_rel arrival counters)
+//   7. depth census           (guards the render kernel's fixed LDS stack)
+#include <hipcub/hipcub.hpp>
+
+#include "gvrt_internal.h"
+
+using namespace gvrt;
+
+namespace {
+
+__device__ inline uint32_t f2ord(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__host__ __device__ inline float ord2f(uint32_t u) {
+    const uint32_t b = (u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u;
+#ifdef __HIP_DEVICE_COMPILE__
+    return __uint_as_float(b);
+#else
+    float f;
+    memcpy(&f, &b, 4);
+    return f;
+#endif
+}
+
+__global__ __launch_bounds__(256) void k_bounds(uint64_t m, const float* __restrict__ boxes,
+                                                uint32_t* __restrict__ out /*6: min xyz, max xyz (ordered)*/) {
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float c = 0.5f * (boxes[6 * i + k] + boxes[6 * i + 3 + k]);
+            lo[k] = fminf(lo[k], c);
+            hi[k] = fmaxf(hi[k], c);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        for (int off = 32; off > 0; off >>= 1) {
+            lo[k] = fminf(lo[k], __shfl_xor(lo[k], off));
+            hi[k] = fmaxf(hi[k], __shfl_xor(hi[k], off));
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            atomicMin(out + k, f2ord(lo[k]));
+            atomicMax(out + 3 + k, f2ord(hi[k]));
+        }
+    }
+}
+
+__device__ inline uint32_t expand10(uint32_t v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_morton(uint64_t m, const float* __restrict__ boxes, const uint32_t* __restrict__ bnd,
+                                                uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    uint32_t code = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float lo = ord2f(bnd[k]), hi = ord2f(bnd[3 + k]);
+        const float c = 0.5f * (boxes[6 * i + k] + boxes[6 * i + 3 + k]);
+        const float ext = hi - lo;
+        float u = ext > 0.0f ? (c - lo) / ext : 0.5f;
+        u = fminf(fmaxf(u * 1024.0f, 0.0f), 1023.0f);
+        code |= expand10((uint32_t)u) << (2 - k);
+    }
+    keys[i] = code;
+    vals[i] = (uint32_t)i;
+}
+
+__global__ __launch_bounds__(256) void k_permute(uint64_t m, const uint32_t* __restrict__ perm, const RenderRec* __restrict__ rin,
+                                                 const float* __restrict__ shin, const float* __restrict__ bin,
+                                                 RenderRec* __restrict__ rout, float* __restrict__ shout,
+                                                 float* __restrict__ bout, uint32_t* __restrict__ leaf_src) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const uint32_t s = perm[j];
+    rout[j] = rin[s];
+    const float4* si = reinterpret_cast<const float4*>(shin + 48ull * s);
+    float4* so = reinterpret_cast<float4*>(shout + 48ull * j);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) so[k] = si[k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) bout[6 * j + k] = bin[6ull * s + k];
+    leaf_src[j] = s;
+}
+
+__device__ inline int delta(const uint32_t* __restrict__ codes, int64_t m, int64_t i, int64_t j) {
+    if (j < 0 || j >= m) return -1;
+    const uint32_t a = codes[i], b = codes[j];
+    if (a == b) return 32 + __clz((uint32_t)(i ^ j));
+    return __clz(a ^ b);
+}
+
+// Karras, "Maximizing Parallelism in the Construction of BVHs, Octrees, and k-d Trees", HPG 2012.
+__global__ __launch_bounds__(256) void k_karras(int64_t m, const uint32_t* __restrict__ codes, BvhNode* __restrict__ nodes,
+                                                int32_t* __restrict__ leaf_parent, int32_t* __restrict__ node_parent) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m - 1) return;
+    const int d = (delta(codes, m, i, i + 1) - delta(codes, m, i, i - 1)) >= 0 ? 1 : -1;
+    const int dmin = delta(codes, m, i, i - d);
+    int64_t lmax = 2;
+    while (delta(codes, m, i, i + lmax * d) > dmin) lmax <<= 1;
+    int64_t l = 0;
+    for (int64_t t = lmax >> 1; t >= 1; t >>= 1)
+        if (delta(codes, m, i, i + (l + t) * d) > dmin) l += t;
+    const int64_t j = i + l * d;
+    const int dnode = delta(codes, m, i, j);
+    int64_t s = 0;
+    int64_t t = l;
+    do {
+        t = (t + 1) >> 1;
+        if (delta(codes, m, i, i + (s + t) * d) > dnode) s += t;
+    } while (t > 1);
+    const int64_t gamma = i + s * d + (d < 0 ? -1 : 0);
+    const int64_t lo = i < j ? i : j, hi = i < j ? j : i;
+    int32_t c0, c1;
+    if (lo == gamma) {
+        c0 = ~(int32_t)gamma;
+        leaf_parent[gamma] = (int32_t)i;
+    } else {
+        c0 = (int32_t)gamma;
+        node_parent[gamma] = (int32_t)i;
+    }
+    if (hi == gamma + 1) {
+        c1 = ~(int32_t)(gamma + 1);
+        leaf_parent[gamma + 1] = (int32_t)i;
+    } else {
+        c1 = (int32_t)(gamma + 1);
+        node_parent[gamma + 1] = (int32_t)i;
+    }
+    nodes[i].c0 = c0;
+    nodes[i].c1 = c1;
+    nodes[i].pad0 = 0;
+    nodes[i].pad1 = 0;
+    if (i == 0) node_parent[0] = -1;
+}
+
+__device__ inline void store_slot(BvhNode* nd, int slot, const float b[6]) {
+    float* f = reinterpret_cast<float*>(nd) + 6 * slot;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) f[k] = b[k];
+}
+
+__global__ __launch_bounds__(256) void k_refit(int64_t m, const float* __restrict__ leaf_boxes, BvhNode* nodes,
+                                               const int32_t* __restrict__ leaf_parent, const int32_t* __restrict__ node_parent,
+                                               uint32_t* counters) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    float b[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) b[k] = leaf_boxes[6 * j + k];
+    int32_t child = ~(int32_t)j;
+    int32_t p = leaf_parent[j];
+    while (p >= 0) {
+        BvhNode* nd = nodes + p;
+        const int slot = (nd->c0 == child) ? 0 : 1;
+        store_slot(nd, slot, b);
+        // release our slot, acquire the sibling's: agent scope (per-XCD L2s are not coherent)
+        const uint32_t old = __hip_atomic_fetch_add(counters + p, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == 0) return;  // first arrival: the sibling's thread continues
+        const float* f = reinterpret_cast<const float*>(nd);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            b[k] = fminf(__hip_atomic_load(f + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                         __hip_atomic_load(f + 6 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            b[3 + k] = fmaxf(__hip_atomic_load(f + 3 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                             __hip_atomic_load(f + 9 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        }
+        child = p;
+        p = node_parent[p];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_depth(int64_t m, const int32_t* __restrict__ leaf_parent,
+                                               const int32_t* __restrict__ node_parent, uint32_t* out) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    uint32_t dpt = 1;
+    int32_t p = leaf_parent[j];
+    while (p >= 0 && dpt < 100000) {
+        ++dpt;
+        p = node_parent[p];
+    }
+    atomicMax(out, dpt);
+}
+
+}  // namespace
+
+gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
+    const int64_t m = (int64_t)c->m;
+    gvrt_dfree(c, (void**)&c->d_recs);
+    gvrt_dfree(c, (void**)&c->d_sh);
+    gvrt_dfree(c, (void**)&c->d_nodes);
+    gvrt_dfree(c, (void**)&c->d_leaf_src);
+    c->accel = false;
+    c->depth = 0;
+    if (m == 0) {
+        c->accel = true;
+        c->stats.bvh_nodes = 0;
+        c->stats.bvh_depth = 0;
+        return GVRT_OK;
+    }
+    if (m > 0x7FFFFFFFll) return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "more than 2^31-1 survivors");
+    gvrt_status s;
+    const int64_t ninternal = m > 1 ? m - 1 : 1;
+    if ((s = gvrt_dalloc(c, (void**)&c->d_recs, sizeof(RenderRec) * m))) return s;
+    if ((s = gvrt_dalloc(c, (void**)&c->d_sh, 192ull * m))) return s;
+    if ((s = gvrt_dalloc(c, (void**)&c->d_nodes, sizeof(BvhNode) * ninternal))) return s;
+    if ((s = gvrt_dalloc(c, (void**)&c->d_leaf_src, 4ull * m))) return s;
+
+    // scratch
+    uint32_t *bnd = nullptr, *keys = nullptr, *vals = nullptr, *keys2 = nullptr, *vals2 = nullptr, *counters = nullptr,
+             *dep = nullptr;
+    int32_t *lpar = nullptr, *npar = nullptr;
+    float* lboxes = nullptr;
+    void* tmp = nullptr;
+    auto cleanup = [&]() {
+        gvrt_dfree(c, (void**)&bnd);
+        gvrt_dfree(c, (void**)&keys);
+        gvrt_dfree(c, (void**)&vals);
+        gvrt_dfree(c, (void**)&keys2);
+        gvrt_dfree(c, (void**)&vals2);
+        gvrt_dfree(c, (void**)&counters);
+        gvrt_dfree(c, (void**)&dep);
+        gvrt_dfree(c, (void**)&lpar);
+        gvrt_dfree(c, (void**)&npar);
+        gvrt_dfree(c, (void**)&lboxes);
+        gvrt_dfree(c, &tmp);
+    };
+#define TRY(x)                   \
+    do {                         \
+        if ((s = (x)) != GVRT_OK) { \
+            cleanup();           \
+            return s;            \
+        }                        \
+    } while (0)
+#define TRYH(x, what)                                   \
+    do {                                                \
+        hipError_t _e = (x);                            \
+        if (_e != hipSuccess) {                         \
+            cleanup();                                  \
+            return gvrt_hip_check(c, _e, what);         \
+        }                                               \
+    } while (0)
+    TRY(gvrt_dalloc(c, (void**)&bnd, 32));
+    TRY(gvrt_dalloc(c, (void**)&keys, 4ull * m));
+    TRY(gvrt_dalloc(c, (void**)&vals, 4ull * m));
+    TRY(gvrt_dalloc(c, (void**)&keys2, 4ull * m));
+    TRY(gvrt_dalloc(c, (void**)&vals2, 4ull * m));
+    TRY(gvrt_dalloc(c, (void**)&counters, 4ull * ninternal));
+    TRY(gvrt_dalloc(c, (void**)&dep, 16));
+    TRY(gvrt_dalloc(c, (void**)&lpar, 4ull * m));
+    TRY(gvrt_dalloc(c, (void**)&npar, 4ull * ninternal));
+    TRY(gvrt_dalloc(c, (void**)&lboxes, 24ull * m));
+
+    TRYH(hipEventRecord(c->ev0, c->stream), "event");
+    const uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
+    TRYH(hipMemcpyAsync(bnd, init, 24, hipMemcpyHostToDevice, c->stream), "bounds init");
+    const unsigned blocks = (unsigned)((m + 255) / 256);
+    const unsigned rblocks = blocks < 2048 ? blocks : 2048;
+    hipLaunchKernelGGL(k_bounds, dim3(rblocks), dim3(256), 0, c->stream, (uint64_t)m, c->d_boxes_c, bnd);
+    hipLaunchKernelGGL(k_morton, dim3(blocks), dim3(256), 0, c->stream, (uint64_t)m, c->d_boxes_c, bnd, keys, vals);
+    TRYH(hipGetLastError(), "k_morton");
+    size_t tmp_bytes = 0;
+    TRYH(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys2, vals, vals2, (int)m, 0, 30, c->stream),
+         "SortPairs size");
+    TRY(gvrt_dalloc(c, &tmp, tmp_bytes ? tmp_bytes : 16));
+    TRYH(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys2, vals, vals2, (int)m, 0, 30, c->stream),
+         "SortPairs");
+    hipLaunchKernelGGL(k_permute, dim3(blocks), dim3(256), 0, c->stream, (uint64_t)m, vals2, c->d_recs_c, c->d_sh48,
+                       c->d_boxes_c, c->d_recs, c->d_sh, lboxes, c->d_leaf_src);
+    TRYH(hipGetLastError(), "k_permute");
+    if (m == 1) {
+        // single proxy: one pseudo-root whose second child is an empty box
+        BvhNode root{};
+        float hb[6];
+        TRYH(hipMemcpyAsync(hb, lboxes, 24, hipMemcpyDeviceToHost, c->stream), "leaf box");
+        TRYH(hipStreamSynchronize(c->stream), "sync");
+        root.l0x = hb[0]; root.l0y = hb[1]; root.l0z = hb[2];
+        root.h0x = hb[3]; root.h0y = hb[4]; root.h0z = hb[5];
+        root.l1x = root.l1y = root.l1z = INFINITY;
+        root.h1x = root.h1y = root.h1z = -INFINITY;
+        root.c0 = ~0;
+        root.c1 = ~0;
+        TRYH(hipMemcpyAsync(c->d_nodes, &root, sizeof(root), hipMemcpyHostToDevice, c->stream), "root");
+        c->depth = 1;
+    } else {
+        TRYH(hipMemsetAsync(counters, 0, 4ull * ninternal, c->stream), "memset");
+        TRYH(hipMemsetAsync(dep, 0, 4, c->stream), "memset");
+        const unsigned iblocks = (unsigned)((m - 1 + 255) / 256);
+        hipLaunchKernelGGL(k_karras, dim3(iblocks), dim3(256), 0, c->stream, m, keys2, c->d_nodes, lpar, npar);
+        hipLaunchKernelGGL(k_refit, dim3(blocks), dim3(256), 0, c->stream, m, lboxes, c->d_nodes, lpar, npar, counters);
+        hipLaunchKernelGGL(k_depth, dim3(blocks), dim3(256), 0, c->stream, m, lpar, npar, dep);
+        TRYH(hipGetLastError(), "k_karras/k_refit");
+        uint32_t hd = 0;
+        TRYH(hipMemcpyAsync(&hd, dep, 4, hipMemcpyDeviceToHost, c->stream), "depth");
+        TRYH(hipStreamSynchronize(c->stream), "sync");
+        c->depth = hd;
+    }
+    TRYH(hipEventRecord(c->ev1, c->stream), "event");
+    TRYH(hipStreamSynchronize(c->stream), "sync");
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
+    c->stats.accel_ms = ms;
+    cleanup();
+#undef TRY
+#undef TRYH
+    if (c->depth + 1 > (uint32_t)STACK_DEPTH)
+        return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "LBVH deeper than the render kernel's traversal stack");
+    c->stats.bvh_nodes = (uint64_t)ninternal;
+    c->stats.bvh_depth = c->depth;
+    c->accel = true;
+    return GVRT_OK;
+}

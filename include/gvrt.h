@@ -1,0 +1,187 @@
+/*
+ * gvrt.h — C-ABI of the MI355X-native Gaussian ray tracer (libgvrt.so).
+ *
+ * This is the drop-in boundary for the Particle Rendering hot path of
+ * wlckslxh/3DGVRT_lightfield (reference snapshot 2025-08-24).  Each entry point names the
+ * reference interface it replaces (paths relative to the reference root).  Plain C types
+ * only: pointers, sizes and POD structs; no HIP or torch types cross this boundary.
+ *
+ * Threading: a handle is bound to one HIP device and one HIP stream and is not thread-safe.
+ * Different handles (one per GPU) may be driven from different threads or processes.
+ * Errors: every call returns a gvrt_status; nothing aborts.  gvrt_last_error() gives text.
+ */
+#ifndef GVRT_H_
+#define GVRT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GVRT_ABI_VERSION 1
+
+typedef int32_t gvrt_status;
+#define GVRT_OK 0
+#define GVRT_ERR_INVALID_ARG (-1)
+#define GVRT_ERR_OOM (-2)
+#define GVRT_ERR_HIP (-3)
+#define GVRT_ERR_STATE (-4)
+#define GVRT_ERR_NO_DEVICE (-5)
+#define GVRT_ERR_IO (-6)
+#define GVRT_ERR_UNSUPPORTED (-7)
+
+typedef struct gvrt_context* gvrt_handle;
+
+/* Host SoA splat arrays, laid out exactly as vk3DGRT::SplatSet
+ * (base/Vulkan3DGRTModel.h:16-28): f_rest already reordered to coefficient-major RGB
+ * (base/Vulkan3DGRTModel.cpp:62-77), rotation stored w,x,y,z. */
+typedef struct {
+    uint64_t n;
+    const float* positions; /* 3n  x,y,z */
+    const float* f_dc;      /* 3n  f_dc_0..2 */
+    const float* f_rest;    /* 45n coefficient-major interleaved RGB */
+    const float* opacity;   /* n   raw logit */
+    const float* scale;     /* 3n  raw log-scale */
+    const float* rotation;  /* 4n  raw quaternion w,x,y,z */
+} gvrt_splats;
+
+/* GaussianEnclosingUniformData (base/VulkanUtils.h:63-68); host defaults from
+ * projects/VulkanFullRT/VulkanFullRT.cpp:1353-1356. */
+typedef struct {
+    float kernel_min_response; /* 0.0113 */
+    uint32_t opts;             /* MOGRenderOpts bit 0 = adaptive kernel clamping; default 0 */
+    float degree;              /* 4 */
+    uint32_t emit_triangles;   /* 1: also keep the 36n vertex / 60n index proxy soup */
+} gvrt_enclosing_params;
+
+/* Render parameters: UniformDataStatic (base/VulkanUtils.h:50-61), the GLSL constants of
+ * shaders/glsl/base/3dgs.glsl:13-22 and the variant switches of SURVEY §8a (Q10, Q11, Q13). */
+typedef struct {
+    float aabb[6];                   /* minX,minY,minZ,maxX,maxY,maxZ = +-100 */
+    float min_transmittance;         /* 0.001 */
+    float hit_min_gaussian_response; /* 0.0113 */
+    uint32_t sph_eval_degree;        /* 3 */
+    float alpha_min;                 /* 1/255 (ALPHA_MIN_THRESHOLD) */
+    float pixel_offset;              /* 0 = ray-query compute variant (default), 0.5 = RT pipeline / LF */
+    float alpha_init;                /* 0 = ray-query variant (default), 1 = RT pipeline / LF */
+    uint32_t tmin_inclusive;         /* 0 (default); 1 only with mode LITERAL and max_rounds > 0 */
+    uint32_t mode;                   /* GVRT_MODE_FAST (default) or GVRT_MODE_LITERAL */
+    uint32_t max_rounds;             /* 0 = unlimited */
+    uint32_t ray_dirs_layout;        /* 0: [cam][y][x]; 1: light-field [cam][x][y] (raygenGaussianLightField.rgen:129) */
+    uint32_t reserved[5];
+} gvrt_render_params;
+
+#define GVRT_MODE_FAST 0u    /* only accepted crossings enter the k-buffer (same image) */
+#define GVRT_MODE_LITERAL 1u /* every crossing enters the 16-slot k-buffer, rounds as the reference */
+
+/* One 8x8 pixel tile of camera `cam` (tile coordinates, not pixels). */
+typedef struct {
+    uint16_t tx, ty;
+    uint16_t cam, pad;
+} gvrt_tile;
+
+/* Output surfaces.  Any pointer may be NULL.  Pointers are device pointers when
+ * device_ptrs = 1, else host pointers (the library stages them). */
+typedef struct {
+    void* rgba8;        /* uint8  [cam][H][W][4]  (R8G8B8A8_UNORM storage image) */
+    float* rgba32f;     /* float  [cam][H][W][4]  (the pre-quantisation rayRadiance) */
+    float* ray_dirs;    /* float4 per ray, layout per params.ray_dirs_layout */
+    uint32_t* hit_counts; /* accepted hits per ray (ENABLE_HIT_COUNTS, raygen.rgen:187-189) */
+    uint32_t device_ptrs;
+    uint32_t packed;      /* 1: outputs are tile-packed in tile-list order (64 px per tile, row-major in tile) */
+} gvrt_image;
+
+typedef struct {
+    uint64_t n_input;      /* N */
+    uint64_t n_survivors;  /* M (ParticleCounts) */
+    uint64_t bvh_nodes;    /* internal nodes */
+    uint32_t bvh_depth;    /* max leaf depth */
+    uint32_t pad0;
+    uint64_t rays;         /* last render */
+    uint64_t crossings;    /* processed crossings (X), last render; only with stats enabled */
+    uint64_t accepted;     /* accepted crossings (A) */
+    uint64_t rounds;       /* sum over rays of k-buffer rounds */
+    float enclose_ms;
+    float accel_ms;
+    float render_ms;       /* device time of the last render kernel (HIP events on the handle's stream) */
+    float pad1;
+    uint64_t device_bytes; /* bytes of device memory held by the handle */
+} gvrt_stats;
+
+/* --------------------------------------------------------------------------------------- */
+int gvrt_abi_version(void);
+const char* gvrt_build_info(void);
+
+void gvrt_default_enclosing_params(gvrt_enclosing_params* p);
+void gvrt_default_render_params(gvrt_render_params* p);
+
+/* VulkanRTBase::initVulkan device pick + VulkanFullRT ctor (base/VulkanRTBase.cpp:1361-1432). */
+gvrt_status gvrt_create(int device, gvrt_handle* out);
+/* VulkanFullRT::~VulkanFullRT (projects/VulkanFullRT/VulkanFullRT.cpp:209-259). */
+gvrt_status gvrt_destroy(gvrt_handle h);
+const char* gvrt_last_error(gvrt_handle h);
+gvrt_status gvrt_device_count(int* count);
+
+/* vk3DGRT::Model::allocateAttributeBuffers (base/Vulkan3DGRTModel.cpp:163-222):
+ * copies the six SoA arrays to device memory. */
+gvrt_status gvrt_load_splats(gvrt_handle h, const gvrt_splats* s);
+
+/* VulkanFullRT::computeGaussianEnclosingIcosaHedron (VulkanFullRT.cpp:1503-1514) dispatching
+ * particlePrimitives.comp; writes the survivor count (ParticleCounts) to *m. */
+gvrt_status gvrt_build_enclosing(gvrt_handle h, const gvrt_enclosing_params* p, uint64_t* m);
+
+/* Read back the enclosing outputs in compaction order (saveIdx): density records 12 f32
+ * (std140 ParticleDensity), SH records 48 f32, and when emit_triangles was set the
+ * 36 f32 vertex / 60 u32 index proxy soup; src_index[i] = input index of survivor i.
+ * Any pointer may be NULL; host pointers; arrays sized for m survivors. */
+gvrt_status gvrt_read_enclosing(gvrt_handle h, float* density12, float* sh48, float* verts36,
+                                uint32_t* tris60, uint32_t* src_index);
+
+/* createBottomLevel/TopLevelAccelerationStructure3DGRT (VulkanFullRT.cpp:575-787):
+ * LBVH (Morton codes, radix sort, Karras hierarchy, AABB refit) over the proxies. */
+gvrt_status gvrt_build_accel(gvrt_handle h);
+
+/* Particle Rendering pass: buildCommandBuffer (VulkanFullRT.cpp:1185-1244) dispatching
+ * raygen/anyhit (RT) or particleRendering.comp (RQ), and the light-field launch
+ * computeGaussianLightField (VulkanFullRT.cpp:1900-1976) when ncams > 1.
+ * view_inverse: ncams column-major 4x4 (UniformDataDynamic.viewInverse per camera);
+ * proj_inverse: one column-major 4x4.  tiles/ntiles: optional 8x8 tile list (multi-GPU
+ * split); NULL renders every tile of every camera.  Synchronous. */
+gvrt_status gvrt_render(gvrt_handle h, const gvrt_render_params* p, const float* view_inverse,
+                        const float* proj_inverse, uint32_t width, uint32_t height,
+                        uint32_t ncams, const gvrt_tile* tiles, uint64_t ntiles,
+                        const gvrt_image* out);
+
+/* Enable per-render statistics (crossings/accepted/rounds; costs one atomic per wave). */
+gvrt_status gvrt_set_stats(gvrt_handle h, int enable);
+gvrt_status gvrt_get_stats(gvrt_handle h, gvrt_stats* s);
+
+/* Scatter a tile-packed rgba8 buffer (gathered from ranks) into a full frame; device ptrs. */
+gvrt_status gvrt_unpack_tiles_rgba8(gvrt_handle h, const void* packed, const gvrt_tile* tiles,
+                                    uint64_t ntiles, uint32_t width, uint32_t height,
+                                    void* frame);
+
+/* --------------------------------------------------------------------------------------- */
+/* Host-side loader: vk3DGRT::PLYLoader::loadPLYModel (base/Vulkan3DGRTModel.cpp:7-125).
+ * Allocates host arrays owned by the returned object; free with gvrt_ply_free. */
+typedef struct {
+    uint64_t n;
+    float* positions;
+    float* f_dc;
+    float* f_rest;
+    float* opacity;
+    float* scale;
+    float* rotation;
+} gvrt_splat_buffers;
+
+gvrt_status gvrt_ply_load(const char* path, gvrt_splat_buffers* out);
+void gvrt_ply_free(gvrt_splat_buffers* b);
+/* Write a binary little-endian 3DGS PLY (inverse of the loader; f_rest written channel-major). */
+gvrt_status gvrt_ply_save(const char* path, const gvrt_splats* s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GVRT_H_ */

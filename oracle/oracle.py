@@ -1,0 +1,144 @@
+"""ctypes wrapper of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module,
+and only as the checker / CPU baseline.  See gvrt_oracle.cpp for what it restates.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+
+class OracleParams(C.Structure):
+    _fields_ = [("aabb", C.c_float * 6), ("min_transmittance", C.c_float), ("hit_min_gaussian_response", C.c_float),
+                ("sph_eval_degree", C.c_uint32), ("alpha_min", C.c_float), ("pixel_offset", C.c_float),
+                ("alpha_init", C.c_float), ("tmin_inclusive", C.c_uint32), ("proxy_mode", C.c_uint32),
+                ("drop_rejected", C.c_uint32), ("max_rounds", C.c_uint32), ("ray_dirs_layout", C.c_uint32),
+                ("kernel_min_response", C.c_float), ("kernel_opts", C.c_uint32), ("kernel_degree", C.c_float)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE, "liboracle.so"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        vp = C.c_void_p
+        L.oracle_enclose.argtypes = [vp] * 6 + [C.c_uint32, C.c_float, C.c_uint32, C.c_float] + [vp] * 6
+        L.oracle_enclose.restype = C.c_int
+        L.oracle_render.argtypes = [vp, vp, vp, vp, C.c_uint32, C.POINTER(OracleParams), vp, vp, C.c_uint32,
+                                    C.c_uint32, C.c_uint32, vp, C.c_uint64, vp, vp, vp, vp, C.c_int]
+        L.oracle_render.restype = C.c_int
+        L.oracle_eval_response.argtypes = [vp] * 5
+        L.oracle_kernel_scale.argtypes = [C.c_float, C.c_float, C.c_uint32, C.c_float]
+        L.oracle_kernel_scale.restype = C.c_float
+        L.oracle_radiance_from_sh.argtypes = [C.c_uint32, vp, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def default_params(**kw):
+    p = OracleParams()
+    p.aabb[:] = [-100.0, -100.0, -100.0, 100.0, 100.0, 100.0]
+    p.min_transmittance = 0.001
+    p.hit_min_gaussian_response = 0.0113
+    p.sph_eval_degree = 3
+    p.alpha_min = 0.0039215686275
+    p.pixel_offset = 0.0
+    p.alpha_init = 0.0
+    p.tmin_inclusive = 0
+    p.proxy_mode = 0
+    p.drop_rejected = 0
+    p.max_rounds = 0
+    p.ray_dirs_layout = 0
+    p.kernel_min_response = 0.0113
+    p.kernel_opts = 0
+    p.kernel_degree = 4.0
+    for k, v in kw.items():
+        if k == "aabb":
+            p.aabb[:] = list(v)
+        else:
+            setattr(p, k, v)
+    return p
+
+
+def enclose(splats, kernel_min_response=0.0113, opts=0, degree=4.0):
+    """particlePrimitives.comp restated; returns dict(verts, tris, density, sh, src_index, m)."""
+    n = splats["positions"].size // 3
+    a = {k: np.ascontiguousarray(splats[k], np.float32) for k in
+         ("positions", "rotation", "scale", "opacity", "f_dc", "f_rest")}
+    verts = np.zeros(36 * max(n, 1), np.float32)
+    tris = np.zeros(60 * max(n, 1), np.uint32)
+    dens = np.zeros(12 * max(n, 1), np.float32)
+    sh = np.zeros(48 * max(n, 1), np.float32)
+    src = np.zeros(max(n, 1), np.uint32)
+    cnt = np.zeros(1, np.uint32)
+    rc = lib().oracle_enclose(_p(a["positions"]), _p(a["rotation"]), _p(a["scale"]), _p(a["opacity"]), _p(a["f_dc"]),
+                              _p(a["f_rest"]), n, kernel_min_response, opts, degree, _p(verts), _p(tris), _p(dens),
+                              _p(sh), _p(cnt), _p(src))
+    assert rc == 0
+    m = int(cnt[0])
+    return {"m": m, "verts": verts[:36 * m], "tris": tris[:60 * m], "density": dens[:12 * m], "sh": sh[:48 * m],
+            "src_index": src[:m]}
+
+
+def render(enc, view_inv, proj_inv, width, height, ncams=1, params=None, subset=None, threads=0, ray_dirs=False,
+           **kw):
+    """Per-ray ray-march restated; returns dict(rgba32f, depth, stats[X, A, rounds], ray_dirs)."""
+    p = params if params is not None else default_params(**kw)
+    vi = np.ascontiguousarray(view_inv, np.float32).reshape(-1)
+    pi = np.ascontiguousarray(proj_inv, np.float32).reshape(16)
+    nr = width * height * ncams if subset is None else len(subset)
+    sub = None if subset is None else np.ascontiguousarray(subset, np.uint64)
+    rgba = np.zeros((nr, 4), np.float32)
+    depth = np.zeros(nr, np.float32)
+    stats = np.zeros((nr, 3), np.uint32)
+    dirs = np.zeros((nr if subset is not None else width * height * ncams, 4), np.float32) if ray_dirs else None
+    rc = lib().oracle_render(_p(enc["verts"]), _p(enc["tris"]), _p(enc["density"]), _p(enc["sh"]), enc["m"],
+                             C.byref(p), _p(vi), _p(pi), width, height, ncams, _p(sub), 0 if sub is None else len(sub),
+                             _p(rgba), _p(depth), _p(dirs), _p(stats), int(threads))
+    assert rc == 0
+    out = {"rgba32f": rgba, "depth": depth, "stats": stats}
+    if ray_dirs:
+        out["ray_dirs"] = dirs
+    if subset is None:
+        out["rgba32f"] = rgba.reshape(ncams, height, width, 4)
+        out["stats"] = stats.reshape(ncams, height, width, 3)
+        out["depth"] = depth.reshape(ncams, height, width)
+    return out
+
+
+def eval_response(density_rec, o, d):
+    g = np.zeros(1, np.float32)
+    a = np.zeros(1, np.float32)
+    lib().oracle_eval_response(_p(np.ascontiguousarray(density_rec, np.float32)), _p(np.asarray(o, np.float32)),
+                               _p(np.asarray(d, np.float32)), _p(g), _p(a))
+    return float(g[0]), float(a[0])
+
+
+def kernel_scale(density, min_response=0.0113, opts=0, degree=4.0):
+    return float(lib().oracle_kernel_scale(density, min_response, opts, degree))
+
+
+def radiance_from_sh(deg, sh48, d):
+    out = np.zeros(3, np.float32)
+    lib().oracle_radiance_from_sh(deg, _p(np.ascontiguousarray(sh48, np.float32)), _p(np.asarray(d, np.float32)),
+                                  _p(out))
+    return out
