@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""Benchmark of the Particle Rendering hot path (BASELINE.json metric: Mrays/s + fps @1920x1080, 1M
+Gaussians; PSNR vs the reference restated by the CPU oracle).
+
+Workload at N=1: config 2 ("bicycle" stand-in, 1M synthetic Gaussians, seed 1, 1920x1080, orbit
+camera r=4 / elev 20 / fovy 50, ray-query variant).  A step = one Particle Rendering pass over one
+1920x1080 view with the scene, proxies and LBVH resident in HBM (enclosing + LBVH build are
+one-shot and reported separately).  With --gpus N each rank renders its own view of an N-camera
+light-field rig (config 5 shards views over GPUs) and the frames are gathered to rank 0 with RCCL
+(torch.distributed 'nccl'): per-GPU work is fixed, so scaling is weak.  `--split tiles` instead
+splits ONE frame into 64x64 blocks round-robin over ranks (strong scaling) and gathers the
+tile-packed parts.
+
+    python bench.py --gpus 1 --steps 20 --warmup 3
+"""
+import argparse
+import importlib
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="bicycle", choices=["bicycle", "garden", "truck", "lightfield", "config1"])
+    ap.add_argument("--split", default="views", choices=["views", "tiles"])
+    ap.add_argument("--mode", default="fast", choices=["fast", "literal"])
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stats", action="store_true", help="skip the LITERAL stats pass (roofline bytes)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        world = max(world, 1)
+    import torch
+    import torch.distributed as dist
+
+    gv = importlib.import_module("3dgvrt_lightfield_amd")
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    gen, W, H, ncams_cfg = gv.scene.CONFIGS[args.config]
+    splats = gv.scene.make(**gen)
+    n_input = splats["positions"].size // 3
+
+    r = gv.Renderer(local_rank)
+    m = r.prepare(splats)
+    st0 = r.stats()
+
+    # cameras: an N-view planar rig around the config-2 orbit camera (view 0 = the config camera)
+    if args.config == "config1":
+        vi0, pi = gv.scene.config1_camera(W, H)
+        eye = np.array([0.0, 0.0, 3.0])
+        target = np.zeros(3)
+        fovy = gv.camera.FOV_Y
+    else:
+        el, az = math.radians(20.0), math.radians(30.0)
+        eye = np.array([4 * math.cos(el) * math.sin(az), 4 * math.sin(el), 4 * math.cos(el) * math.cos(az)])
+        target = np.zeros(3)
+        fovy = 50.0
+    views = world if args.split == "views" else 1
+    views = max(views, ncams_cfg if args.config == "lightfield" else 1)
+    vis, pi = gv.camera.lightfield_grid_rig(eye, target, (0.0, 1.0, 0.0), nx=views, ny=1, spacing=0.1,
+                                            fovy_deg=fovy, aspect=W / H)
+    vis = vis.reshape(views, 16)
+    if args.split == "views":
+        my_views = [v for v in range(views) if v % world == rank]
+        vi = np.ascontiguousarray(vis[my_views].reshape(-1))
+        ncams = len(my_views)
+        tiles = None
+        rays_per_rank = W * H * ncams
+        frame = torch.zeros((ncams, H, W, 4), dtype=torch.uint8, device=dev)
+    else:
+        vi = np.ascontiguousarray(vis[0])
+        ncams = 1
+        tiles = gv.tiles_for_rank(W, H, 1, rank, world, block=8)
+        rays_per_rank = int(tiles.shape[0]) * 64
+        frame = torch.zeros((tiles.shape[0] * 64, 4), dtype=torch.uint8, device=dev)
+    mode = gv.MODE_FAST if args.mode == "fast" else gv.MODE_LITERAL
+    params = r.render_params(mode=mode)
+
+    gathered = None
+    if distributed and rank == 0:
+        if args.split == "views":
+            gathered = [torch.empty_like(frame) for _ in range(world)]
+        else:
+            sizes = [gv.tiles_for_rank(W, H, 1, q, world, block=8).shape[0] * 64 for q in range(world)]
+            gathered = [torch.empty((s, 4), dtype=torch.uint8, device=dev) for s in sizes]
+    if distributed and args.split == "tiles":
+        # NCCL gather needs equal sizes: pad every rank's part to the largest
+        maxs = max(gv.tiles_for_rank(W, H, 1, q, world, block=8).shape[0] for q in range(world)) * 64
+        sendbuf = torch.zeros((maxs, 4), dtype=torch.uint8, device=dev)
+        if rank == 0:
+            gathered = [torch.empty((maxs, 4), dtype=torch.uint8, device=dev) for _ in range(world)]
+
+    kernel_ms = []
+
+    def step():
+        r.render_device(vi, pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=frame.data_ptr(),
+                        packed=args.split == "tiles")
+        kernel_ms.append(r.stats()["render_ms"])
+        if distributed:
+            if args.split == "views":
+                dist.gather(frame, gathered if rank == 0 else None, dst=0)
+            else:
+                sendbuf[: frame.shape[0]].copy_(frame)
+                dist.gather(sendbuf, gathered if rank == 0 else None, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    kernel_ms.clear()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        rays_t = torch.tensor([rays_per_rank], dtype=torch.float64, device=dev)
+        dist.all_reduce(rays_t)
+        total_rays_per_step = float(rays_t.item())
+    else:
+        total_rays_per_step = float(rays_per_rank)
+
+    ms_per_step = elapsed / args.steps * 1e3
+    mrays = total_rays_per_step * args.steps / elapsed / 1e6
+    kern_avg = float(np.mean(kernel_ms)) if kernel_ms else float("nan")
+
+    result = None
+    if rank == 0:
+        # ---- roofline: algorithmic bytes of the reference algorithm on this input (LITERAL counters)
+        roof = None
+        lit_stats = None
+        if not args.no_stats:
+            r.set_stats(True)
+            r.render(vi[:16], pi, W, H, 1, params=r.render_params(mode=gv.MODE_LITERAL), rgba8=False, rgba32f=False)
+            lit_stats = r.stats()
+            r.set_stats(False)
+            rays1 = W * H
+            bytes_per_launch = (48.0 * lit_stats["crossings"] + 192.0 * lit_stats["accepted"] + 4.0 * rays1) * (
+                rays_per_rank / rays1)
+            achieved = bytes_per_launch / (kern_avg * 1e-3) / 1e9
+            traffic = None
+            pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+            if os.path.exists(pmc):
+                try:
+                    traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+                except Exception:
+                    traffic = None
+            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                    "algorithmic_bytes_per_launch": bytes_per_launch,
+                    "kernel_ms_avg": round(kern_avg, 4), "kernel": "k_render<false,false>"}
+
+        # ---- CPU baseline (oracle restatement, all host threads we use), PSNR vs oracle on the sample
+        cpu = None
+        psnr = None
+        if not args.no_cpu_baseline and world == 1:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O
+
+            threads = min(16, os.cpu_count() or 1)
+            e = O.enclose(splats)
+            sc = O.Scene(e, proxy_mode=1)
+            probe = np.arange(0, W * H, 2003, dtype=np.uint64)
+            t = time.perf_counter()
+            sc.render(vi[:16], pi, W, H, subset=probe, threads=threads)
+            rate = len(probe) / max(time.perf_counter() - t, 1e-6)
+            nsub = int(min(W * H, max(len(probe), rate * args.cpu_seconds)))
+            stride = max(1, (W * H) // nsub)
+            sub = np.arange(0, W * H, stride, dtype=np.uint64)
+            t = time.perf_counter()
+            ref = sc.render(vi[:16], pi, W, H, subset=sub, threads=threads)
+            dt = time.perf_counter() - t
+            cpu = {"value": round(len(sub) / dt / 1e6, 6), "unit": "Mrays/s", "cores": threads, "kind": "port",
+                   "sample": f"{len(sub)} rays (every {stride}th pixel of view 0), oracle analytic-proxy literal "
+                             f"ray-march, {dt:.1f} s on {threads} threads"}
+            img = r.render(vi[:16], pi, W, H, 1, params=params, rgba32f=True, rgba8=True)
+            got = img["rgba8"].reshape(-1, 4)[sub.astype(np.int64)]
+            psnr = gv.psnr_rgb(got, gv.quantize_rgba8(ref["rgba32f"]))
+
+        result = {
+            "metric": "Mrays/s + fps @1920x1080, 1M Gaussians; PSNR vs Vulkan reference",
+            "value": round(mrays, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak" if args.split == "views" else "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded stand-in scene, SURVEY §8d)",
+            "config": {"workload": f"{args.config}: {n_input} synthetic Gaussians, {W}x{H}, "
+                                   f"{'one view per rank' if args.split == 'views' else 'one frame tile-split'}, "
+                                   f"ray-query variant, {args.mode} k-buffer",
+                       "gaussians": n_input, "survivors": m, "width": W, "height": H,
+                       "views": views, "split": args.split, "parallelism": f"{args.split}{world}"},
+            "fps": round(1e3 / ms_per_step, 2),
+            "kernel_ms": round(kern_avg, 4),
+            "kernel_mrays": round(rays_per_rank / (kern_avg * 1e-3) / 1e6, 3) if kern_avg == kern_avg else None,
+            "psnr_vs_oracle_db": None if psnr is None else (round(psnr, 2) if math.isfinite(psnr) else "inf"),
+            "enclose_ms": round(st0["enclose_ms"], 3),
+            "accel_ms": round(st0["accel_ms"], 3),
+            "bvh_depth": st0["bvh_depth"],
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        if lit_stats:
+            result["reference_counters"] = {"crossings_per_ray": lit_stats["crossings"] / (W * H),
+                                            "accepted_per_ray": lit_stats["accepted"] / (W * H),
+                                            "rounds_per_ray": lit_stats["rounds"] / (W * H)}
+        print(json.dumps(result), flush=True)
+    r.close()
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

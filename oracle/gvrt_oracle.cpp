@@ -348,7 +348,7 @@ void buildBvh(const std::vector<float>& boxes /*6 per item*/, uint32_t n, Bvh& b
 }
 
 // conservative slab test against [t0, t1]
-inline bool boxHit(const BNode& n, V3 o, V3 inv, float t0, float t1) {
+inline bool boxHit(const BNode& n, V3 o, V3 inv, float t0, float t1, float* tenter = nullptr) {
     float tn = t0, tf = t1;
     for (int k = 0; k < 3; ++k) {
         const float ok = comp(o, k), ik = comp(inv, k);
@@ -361,6 +361,7 @@ inline bool boxHit(const BNode& n, V3 o, V3 inv, float t0, float t1) {
         tn = std::max(tn, a - pad);
         tf = std::min(tf, b + pad);
     }
+    if (tenter) *tenter = tn;
     return tn <= tf;
 }
 
@@ -543,14 +544,27 @@ struct Hit {
 
 // The per-ray ray-march: particleRendering.comp:117-191 (RQ) / raygen.rgen:303-383 (RT).
 // out_stats[3*r] = processed crossings (X_r), [3r+1] = accepted (A_r), [3r+2] = rounds.
-int oracle_render(const float* verts, const uint32_t* tris, const float* density, const float* sh,
-                  uint32_t M, const oracle_params* P, const float* viewInverse,
-                  const float* projInverse, uint32_t W, uint32_t H, uint32_t ncams,
-                  const uint64_t* subset, uint64_t nsubset, float* out_rgba, float* out_depth,
-                  float* out_ray_dirs, uint32_t* out_stats, int nthreads) {
-    if (!P || !density || !sh || !viewInverse || !projInverse || !out_rgba) return -1;
-    if (P->proxy_mode == 0 && (!verts || !tris)) return -1;
-    Scene s{verts, tris, density, sh, M, {}};
+struct OracleScene {
+    Scene s;
+    Bvh bvh;
+    uint32_t proxy_mode;
+};
+
+// Acceleration structure of the oracle (the driver BLAS/TLAS build is not restated; any
+// correct BVH yields the same k-nearest sets).  Input arrays must outlive the scene.
+void* oracle_scene_create(const float* verts, const uint32_t* tris, const float* density, const float* sh,
+                          uint32_t M, uint32_t proxy_mode, float kernel_min_response, uint32_t kernel_opts,
+                          float kernel_degree) {
+    if (!density || !sh) return nullptr;
+    if (proxy_mode == 0 && (!verts || !tris)) return nullptr;
+    OracleScene* os = new OracleScene{Scene{verts, tris, density, sh, M, {}}, Bvh{}, proxy_mode};
+    Scene& s = os->s;
+    oracle_params kp{};
+    kp.kernel_min_response = kernel_min_response;
+    kp.kernel_opts = kernel_opts;
+    kp.kernel_degree = kernel_degree;
+    kp.proxy_mode = proxy_mode;
+    const oracle_params* P = &kp;
     // proxy boxes
     std::vector<float> boxes(6ull * M);
     if (P->proxy_mode == 1) {
@@ -587,8 +601,22 @@ int oracle_render(const float* verts, const uint32_t* tris, const float* density
             }
         }
     }
-    Bvh bvh;
-    buildBvh(boxes, M, bvh);
+    buildBvh(boxes, M, os->bvh);
+    return os;
+}
+
+void oracle_scene_destroy(void* h) { delete static_cast<OracleScene*>(h); }
+
+int oracle_scene_render(void* h, const oracle_params* P, const float* viewInverse, const float* projInverse,
+                        uint32_t W, uint32_t H, uint32_t ncams, const uint64_t* subset, uint64_t nsubset,
+                        float* out_rgba, float* out_depth, float* out_ray_dirs, uint32_t* out_stats, int nthreads) {
+    OracleScene* os = static_cast<OracleScene*>(h);
+    if (!os || !P || !viewInverse || !projInverse || !out_rgba) return -1;
+    if (P->proxy_mode != os->proxy_mode) return -2;
+    const Scene& s = os->s;
+    const Bvh& bvh = os->bvh;
+    const float* verts = s.verts;
+    const uint32_t* tris = s.tris;
 
     const uint64_t nrays_full = (uint64_t)W * H * ncams;
     const uint64_t nwork = subset ? nsubset : nrays_full;
@@ -655,8 +683,18 @@ int oracle_render(const float* verts, const uint32_t* tris, const float* density
                                         : tmax;
                 if (!boxHit(nd, o, inv, tmin, tcull)) continue;
                 if (nd.count == 0) {
-                    stack.push_back(nd.left + 1);
-                    stack.push_back(nd.left);
+                    // front-to-back: pop the nearer child first (culling only; results unchanged)
+                    float e0 = INFINITY, e1 = INFINITY;
+                    const bool h0 = boxHit(bvh.nodes[nd.left], o, inv, tmin, tcull, &e0);
+                    const bool h1 = boxHit(bvh.nodes[nd.left + 1], o, inv, tmin, tcull, &e1);
+                    if (h0 && h1) {
+                        stack.push_back(e0 <= e1 ? nd.left + 1 : nd.left);
+                        stack.push_back(e0 <= e1 ? nd.left : nd.left + 1);
+                    } else if (h0) {
+                        stack.push_back(nd.left);
+                    } else if (h1) {
+                        stack.push_back(nd.left + 1);
+                    }
                     continue;
                 }
                 for (uint32_t k = 0; k < nd.count; ++k) {
@@ -712,6 +750,21 @@ int oracle_render(const float* verts, const uint32_t* tris, const float* density
         }
     }
     return 0;
+}
+
+int oracle_render(const float* verts, const uint32_t* tris, const float* density, const float* sh,
+                  uint32_t M, const oracle_params* P, const float* viewInverse,
+                  const float* projInverse, uint32_t W, uint32_t H, uint32_t ncams,
+                  const uint64_t* subset, uint64_t nsubset, float* out_rgba, float* out_depth,
+                  float* out_ray_dirs, uint32_t* out_stats, int nthreads) {
+    if (!P) return -1;
+    void* h = oracle_scene_create(verts, tris, density, sh, M, P->proxy_mode, P->kernel_min_response,
+                                  P->kernel_opts, P->kernel_degree);
+    if (!h) return -1;
+    const int rc = oracle_scene_render(h, P, viewInverse, projInverse, W, H, ncams, subset, nsubset, out_rgba,
+                                       out_depth, out_ray_dirs, out_stats, nthreads);
+    oracle_scene_destroy(h);
+    return rc;
 }
 
 // Single-Gaussian response helper for known-answer tests.

@@ -42,6 +42,12 @@ def lib():
         L.oracle_render.argtypes = [vp, vp, vp, vp, C.c_uint32, C.POINTER(OracleParams), vp, vp, C.c_uint32,
                                     C.c_uint32, C.c_uint32, vp, C.c_uint64, vp, vp, vp, vp, C.c_int]
         L.oracle_render.restype = C.c_int
+        L.oracle_scene_create.argtypes = [vp, vp, vp, vp, C.c_uint32, C.c_uint32, C.c_float, C.c_uint32, C.c_float]
+        L.oracle_scene_create.restype = vp
+        L.oracle_scene_destroy.argtypes = [vp]
+        L.oracle_scene_render.argtypes = [vp, C.POINTER(OracleParams), vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp,
+                                          C.c_uint64, vp, vp, vp, vp, C.c_int]
+        L.oracle_scene_render.restype = C.c_int
         L.oracle_eval_response.argtypes = [vp] * 5
         L.oracle_kernel_scale.argtypes = [C.c_float, C.c_float, C.c_uint32, C.c_float]
         L.oracle_kernel_scale.restype = C.c_float
@@ -142,3 +148,37 @@ def radiance_from_sh(deg, sh48, d):
     lib().oracle_radiance_from_sh(deg, _p(np.ascontiguousarray(sh48, np.float32)), _p(np.asarray(d, np.float32)),
                                   _p(out))
     return out
+
+
+class Scene:
+    """Persistent oracle scene (BVH built once); render() times only the per-ray ray-march."""
+
+    def __init__(self, enc, proxy_mode=1, kernel_min_response=0.0113, opts=0, degree=4.0):
+        self.enc = enc  # keep arrays alive
+        self.proxy_mode = proxy_mode
+        self.kw = dict(kernel_min_response=kernel_min_response, kernel_opts=opts, kernel_degree=degree)
+        self.h = lib().oracle_scene_create(_p(enc["verts"]) if proxy_mode == 0 else None,
+                                           _p(enc["tris"]) if proxy_mode == 0 else None, _p(enc["density"]),
+                                           _p(enc["sh"]), enc["m"], proxy_mode, kernel_min_response, opts, degree)
+        assert self.h
+
+    def close(self):
+        if self.h:
+            lib().oracle_scene_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def render(self, view_inv, proj_inv, width, height, ncams=1, subset=None, threads=0, **kw):
+        p = default_params(proxy_mode=self.proxy_mode, **self.kw, **kw)
+        vi = np.ascontiguousarray(view_inv, np.float32).reshape(-1)
+        pi = np.ascontiguousarray(proj_inv, np.float32).reshape(16)
+        nr = width * height * ncams if subset is None else len(subset)
+        sub = None if subset is None else np.ascontiguousarray(subset, np.uint64)
+        rgba = np.zeros((nr, 4), np.float32)
+        stats = np.zeros((nr, 3), np.uint32)
+        rc = lib().oracle_scene_render(self.h, C.byref(p), _p(vi), _p(pi), width, height, ncams, _p(sub),
+                                       0 if sub is None else len(sub), _p(rgba), None, None, _p(stats), int(threads))
+        assert rc == 0, rc
+        return {"rgba32f": rgba, "stats": stats}
