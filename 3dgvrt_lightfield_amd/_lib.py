@@ -47,7 +47,7 @@ class RenderParams(C.Structure):
                 ("hit_min_gaussian_response", C.c_float), ("sph_eval_degree", C.c_uint32),
                 ("alpha_min", C.c_float), ("pixel_offset", C.c_float), ("alpha_init", C.c_float),
                 ("tmin_inclusive", C.c_uint32), ("mode", C.c_uint32), ("max_rounds", C.c_uint32),
-                ("ray_dirs_layout", C.c_uint32), ("reserved", C.c_uint32 * 5)]
+                ("ray_dirs_layout", C.c_uint32), ("kbuffer_depth", C.c_uint32), ("reserved", C.c_uint32 * 4)]
 
 
 class Tile(C.Structure):
@@ -64,7 +64,8 @@ class Stats(C.Structure):
                 ("bvh_depth", C.c_uint32), ("pad0", C.c_uint32), ("rays", C.c_uint64),
                 ("crossings", C.c_uint64), ("accepted", C.c_uint64), ("rounds", C.c_uint64),
                 ("enclose_ms", C.c_float), ("accel_ms", C.c_float), ("render_ms", C.c_float),
-                ("pad1", C.c_float), ("device_bytes", C.c_uint64)]
+                ("pad1", C.c_float), ("device_bytes", C.c_uint64), ("wave_node_visits", C.c_uint64),
+                ("wave_leaf_visits", C.c_uint64), ("lane_leaf_tests", C.c_uint64)]
 
 
 H = C.c_void_p

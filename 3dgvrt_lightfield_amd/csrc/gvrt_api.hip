@@ -280,9 +280,8 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
     std::memset(&a, 0, sizeof(a));
     a.recs = c->d_recs;
     a.sh = c->d_sh;
-    a.nodes = c->d_nodes;
+    a.nodes = c->d_nodes4;
     a.nrecs = (uint32_t)c->m;
-    a.root_is_leaf = c->m == 1 ? 1u : 0u;
     // cameras
     if ((s = ensure(c, (void**)&c->d_viewinv, &c->viewinv_cap, 64ull * ncams))) return s;
     GVRT_HIP(c, hipMemcpyAsync(c->d_viewinv, view_inverse, 64ull * ncams, hipMemcpyHostToDevice, c->stream));
@@ -308,6 +307,9 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
     a.max_rounds = p->max_rounds;
     a.ray_dirs_layout = p->ray_dirs_layout;
     a.packed = out->packed;
+    a.kfast = p->kbuffer_depth ? p->kbuffer_depth : (uint32_t)K_HITS;
+    if (a.kfast != 8 && a.kfast != 12 && a.kfast != 16 && a.kfast != 24)
+        return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "kbuffer_depth must be 0, 8, 12, 16 or 24");
     uint64_t nwork = total_tiles;
     if (tiles) {
         std::vector<uint32_t> tl(ntiles);
@@ -349,7 +351,7 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
         }
     }
     if (c->stats_on) {
-        GVRT_HIP(c, hipMemsetAsync(c->d_stats, 0, 24, c->stream));
+        GVRT_HIP(c, hipMemsetAsync(c->d_stats, 0, 48, c->stream));
         a.stats = c->d_stats;
     }
     GVRT_HIP(c, hipEventRecord(c->ev0, c->stream));
@@ -361,8 +363,8 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
         if (bhc) GVRT_HIP(c, hipMemcpyAsync(out->hit_counts, a.hit_counts, bhc, hipMemcpyDeviceToHost, c->stream));
         if (b8) GVRT_HIP(c, hipMemcpyAsync(out->rgba8, a.rgba8, b8, hipMemcpyDeviceToHost, c->stream));
     }
-    unsigned long long hs[3] = {0, 0, 0};
-    if (c->stats_on) GVRT_HIP(c, hipMemcpyAsync(hs, c->d_stats, 24, hipMemcpyDeviceToHost, c->stream));
+    unsigned long long hs[6] = {0, 0, 0, 0, 0, 0};
+    if (c->stats_on) GVRT_HIP(c, hipMemcpyAsync(hs, c->d_stats, 48, hipMemcpyDeviceToHost, c->stream));
     GVRT_HIP(c, hipStreamSynchronize(c->stream));
     float ms = 0.f;
     GVRT_HIP(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
@@ -371,6 +373,9 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
     c->stats.crossings = hs[0];
     c->stats.accepted = hs[1];
     c->stats.rounds = hs[2];
+    c->stats.wave_node_visits = hs[3];
+    c->stats.wave_leaf_visits = hs[4];
+    c->stats.lane_leaf_tests = hs[5];
     return GVRT_OK;
 }
 

@@ -41,6 +41,19 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 B");
 
+// 4-wide node collapsed from the binary LBVH (every even-depth binary node becomes one node whose
+// children are its children or grandchildren).  SoA inside the node so one lane-uniform pair of
+// s_load_dwordx16 brings all four boxes.  Empty slots hold a far point box that no ray can hit.
+constexpr int BVH_W = 4;
+constexpr float EMPTY_BOX = 3e37f;
+struct alignas(16) Bvh4Node {
+    float lox[4], loy[4], loz[4];
+    float hix[4], hiy[4], hiz[4];
+    int32_t child[4];  // >= 0: Bvh4Node index; < 0: leaf ~record index
+    uint32_t nchild, pad[3];
+};
+static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node must be 128 B");
+
 struct f3 {
     float x, y, z;
 };
@@ -58,7 +71,7 @@ __host__ __device__ inline f3 cross3(f3 a, f3 b) {
 struct RenderArgs {
     const RenderRec* __restrict__ recs;
     const float* __restrict__ sh;        // 48 f32 per record
-    const BvhNode* __restrict__ nodes;
+    const Bvh4Node* __restrict__ nodes;
     const float* __restrict__ view_inv;  // 16 per camera, column-major
     const uint32_t* __restrict__ tiles;  // packed (cam<<24 | ty<<12 | tx) or null
     float proj_inv[16];
@@ -81,7 +94,7 @@ struct RenderArgs {
     uint32_t max_rounds;
     uint32_t ray_dirs_layout;
     uint32_t packed;
-    uint32_t root_is_leaf;   // M == 1
+    uint32_t kfast;  // FAST-mode k-buffer depth (8, 12, 16, 24)
     uint8_t* rgba8;
     float* rgba32f;
     float* ray_dirs;

@@ -44,7 +44,9 @@ struct gvrt_context {
     bool accel = false;
     gvrt::RenderRec* d_recs = nullptr;
     float* d_sh = nullptr;
-    gvrt::BvhNode* d_nodes = nullptr;
+    gvrt::BvhNode* d_nodes = nullptr;   // binary LBVH (kept for diagnostics)
+    gvrt::Bvh4Node* d_nodes4 = nullptr; // 4-wide collapse traversed by the render kernel
+    uint64_t n_nodes4 = 0;
     uint32_t* d_leaf_src = nullptr;  // leaf -> compaction index
     uint32_t depth = 0;
 

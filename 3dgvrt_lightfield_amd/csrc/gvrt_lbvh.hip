@@ -205,6 +205,63 @@ __global__ __launch_bounds__(256) void k_depth(int64_t m, const int32_t* __restr
     atomicMax(out, dpt);
 }
 
+// even-depth flags of binary internal nodes (root depth 0): each becomes one 4-wide node
+__global__ __launch_bounds__(256) void k_even_flags(int64_t ni, const int32_t* __restrict__ node_parent,
+                                                    uint32_t* __restrict__ flags) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > ni) return;
+    if (i == ni) {
+        flags[i] = 0;
+        return;
+    }
+    uint32_t dpt = 0;
+    int32_t p = node_parent[i];
+    while (p >= 0 && dpt < 100000) {
+        ++dpt;
+        p = node_parent[p];
+    }
+    flags[i] = (dpt & 1u) == 0 ? 1u : 0u;
+}
+
+__device__ inline void put_slot(Bvh4Node& o, int k, const float* b, int32_t ref) {
+    o.lox[k] = b[0]; o.loy[k] = b[1]; o.loz[k] = b[2];
+    o.hix[k] = b[3]; o.hiy[k] = b[4]; o.hiz[k] = b[5];
+    o.child[k] = ref;
+}
+
+// Collapse: an even-depth node keeps a leaf child as is and replaces an internal child (odd depth)
+// by that child's two children (leaves or even-depth nodes).
+__global__ __launch_bounds__(256) void k_collapse(int64_t ni, const BvhNode* __restrict__ nodes,
+                                                  const uint32_t* __restrict__ flags, const uint32_t* __restrict__ idx4,
+                                                  Bvh4Node* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ni || !flags[i]) return;
+    const BvhNode n = nodes[i];
+    Bvh4Node o;
+    int k = 0;
+    const float* nb = reinterpret_cast<const float*>(&n);
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+        const int32_t c = side ? n.c1 : n.c0;
+        if (c < 0) {
+            put_slot(o, k++, nb + 6 * side, c);
+        } else {
+            const BvhNode g = nodes[c];
+            const float* gb = reinterpret_cast<const float*>(&g);
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int32_t gc = s2 ? g.c1 : g.c0;
+                put_slot(o, k++, gb + 6 * s2, gc < 0 ? gc : (int32_t)idx4[gc]);
+            }
+        }
+    }
+    const float eb[6] = {EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX};
+    o.nchild = (uint32_t)k;
+    for (; k < 4; ++k) put_slot(o, k, eb, 0);
+    o.pad[0] = o.pad[1] = o.pad[2] = 0;
+    out[idx4[i]] = o;
+}
+
 }  // namespace
 
 gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
@@ -212,7 +269,9 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
     gvrt_dfree(c, (void**)&c->d_recs);
     gvrt_dfree(c, (void**)&c->d_sh);
     gvrt_dfree(c, (void**)&c->d_nodes);
+    gvrt_dfree(c, (void**)&c->d_nodes4);
     gvrt_dfree(c, (void**)&c->d_leaf_src);
+    c->n_nodes4 = 0;
     c->accel = false;
     c->depth = 0;
     if (m == 0) {
@@ -292,18 +351,21 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
                        c->d_boxes_c, c->d_recs, c->d_sh, lboxes, c->d_leaf_src);
     TRYH(hipGetLastError(), "k_permute");
     if (m == 1) {
-        // single proxy: one pseudo-root whose second child is an empty box
-        BvhNode root{};
+        // single proxy: one 4-wide root with one leaf slot
+        Bvh4Node root{};
         float hb[6];
         TRYH(hipMemcpyAsync(hb, lboxes, 24, hipMemcpyDeviceToHost, c->stream), "leaf box");
         TRYH(hipStreamSynchronize(c->stream), "sync");
-        root.l0x = hb[0]; root.l0y = hb[1]; root.l0z = hb[2];
-        root.h0x = hb[3]; root.h0y = hb[4]; root.h0z = hb[5];
-        root.l1x = root.l1y = root.l1z = INFINITY;
-        root.h1x = root.h1y = root.h1z = -INFINITY;
-        root.c0 = ~0;
-        root.c1 = ~0;
-        TRYH(hipMemcpyAsync(c->d_nodes, &root, sizeof(root), hipMemcpyHostToDevice, c->stream), "root");
+        for (int k = 0; k < 4; ++k) {
+            const float* b = k == 0 ? hb : nullptr;
+            root.lox[k] = b ? b[0] : EMPTY_BOX; root.loy[k] = b ? b[1] : EMPTY_BOX; root.loz[k] = b ? b[2] : EMPTY_BOX;
+            root.hix[k] = b ? b[3] : EMPTY_BOX; root.hiy[k] = b ? b[4] : EMPTY_BOX; root.hiz[k] = b ? b[5] : EMPTY_BOX;
+            root.child[k] = k == 0 ? ~0 : 0;
+        }
+        root.nchild = 1;
+        TRY(gvrt_dalloc(c, (void**)&c->d_nodes4, sizeof(Bvh4Node)));
+        TRYH(hipMemcpyAsync(c->d_nodes4, &root, sizeof(root), hipMemcpyHostToDevice, c->stream), "root");
+        c->n_nodes4 = 1;
         c->depth = 1;
     } else {
         TRYH(hipMemsetAsync(counters, 0, 4ull * ninternal, c->stream), "memset");
@@ -315,8 +377,27 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
         TRYH(hipGetLastError(), "k_karras/k_refit");
         uint32_t hd = 0;
         TRYH(hipMemcpyAsync(&hd, dep, 4, hipMemcpyDeviceToHost, c->stream), "depth");
+        // ---- collapse to the 4-wide tree (reuse keys/vals as flags / scan)
+        const int64_t ni = m - 1;
+        hipLaunchKernelGGL(k_even_flags, dim3((unsigned)((ni + 1 + 255) / 256)), dim3(256), 0, c->stream, ni, npar,
+                           keys);
+        size_t sb = 0;
+        TRYH(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, keys, vals, (int)(ni + 1), c->stream), "scan size");
+        if (sb > tmp_bytes) {
+            gvrt_dfree(c, &tmp);
+            TRY(gvrt_dalloc(c, &tmp, sb));
+            tmp_bytes = sb;
+        }
+        TRYH(hipcub::DeviceScan::ExclusiveSum(tmp, sb, keys, vals, (int)(ni + 1), c->stream), "scan");
+        uint32_t n4 = 0;
+        TRYH(hipMemcpyAsync(&n4, vals + ni, 4, hipMemcpyDeviceToHost, c->stream), "n4");
         TRYH(hipStreamSynchronize(c->stream), "sync");
         c->depth = hd;
+        TRY(gvrt_dalloc(c, (void**)&c->d_nodes4, sizeof(Bvh4Node) * (n4 ? n4 : 1)));
+        hipLaunchKernelGGL(k_collapse, dim3((unsigned)((ni + 255) / 256)), dim3(256), 0, c->stream, ni, c->d_nodes,
+                           keys, vals, c->d_nodes4);
+        TRYH(hipGetLastError(), "k_collapse");
+        c->n_nodes4 = n4;
     }
     TRYH(hipEventRecord(c->ev1, c->stream), "event");
     TRYH(hipStreamSynchronize(c->stream), "sync");
@@ -326,9 +407,10 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
     cleanup();
 #undef TRY
 #undef TRYH
-    if (c->depth + 1 > (uint32_t)STACK_DEPTH)
+    // the 4-wide traversal pushes at most 3 entries per 4-wide level
+    if (3 * ((c->depth + 1) / 2) + 2 > (uint32_t)STACK_DEPTH)
         return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "LBVH deeper than the render kernel's traversal stack");
-    c->stats.bvh_nodes = (uint64_t)ninternal;
+    c->stats.bvh_nodes = c->n_nodes4;
     c->stats.bvh_depth = c->depth;
     c->accel = true;
     return GVRT_OK;

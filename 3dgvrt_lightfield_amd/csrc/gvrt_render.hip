@@ -6,22 +6,26 @@
 // traversal behind traceRayEXT / rayQueryProceedEXT.
 //
 // Mapping to CDNA4: one wave64 = one 8x8 pixel tile (one lane per ray), four tiles per
-// 256-thread workgroup.  Traversal is wave-uniform (packet traversal): node and leaf records
-// are addressed by a wave-uniform index and fetched with scalar loads (one s_load_dwordx16 per
-// 64-B node / record), every lane clips its own ray against both child boxes, and a ballot
-// decides which children the packet descends into; the far child goes on a per-wave LDS stack.
-// Leaves are clipped against the analytic icosahedron (10 antipodal slab pairs in the kernel
-// frame), which yields the same two crossings (entry and exit face, Q1) as the reference's
-// 20-triangle proxy.  Each lane keeps a 16-slot register k-buffer (compareAndSwapHitPayloadValue
-// chain, anyhit.rahit:29-71); a full buffer shrinks that lane's culling distance as the
-// driver's tmax does.  After each traversal round every lane composites its hits front to back
-// (processHit, gaussianfunctions.glsl:153-229) with the SH basis of its ray direction
-// precomputed once per ray (the reference's scalar basis factors, same summation order).
+// 256-thread workgroup.  Traversal is wave-uniform (packet traversal) over the 4-wide collapse of
+// the LBVH: node and leaf records are addressed by a wave-uniform index and fetched with scalar
+// loads (two s_load_dwordx16 per 128-B node, one per 64-B record), every lane clips its own ray
+// against the four child boxes, and ballots decide which children the packet descends into; the
+// farther children go on a per-wave LDS stack, nearest first by the first hitting lane's entry
+// distance.  Leaves are clipped against the analytic icosahedron (10 antipodal slab pairs in the
+// kernel frame), which yields the same two crossings (entry and exit face, Q1) as the
+// reference's 20-triangle proxy.  Each lane keeps a 16-slot register k-buffer
+// (compareAndSwapHitPayloadValue chain, anyhit.rahit:29-71); a full buffer shrinks that lane's
+// culling distance as the driver's tmax does.  After each traversal round every lane composites
+// its hits front to back (processHit, gaussianfunctions.glsl:153-229) with the SH basis of its
+// ray direction precomputed once per ray (the reference's scalar basis factors, same order).
 //
 // Modes: LITERAL = every crossing enters the k-buffer, rounds exactly as the reference
 // (16 per trace, `last` advanced by rejected hits too).  FAST = only accepted crossings enter the
 // k-buffer; with an exclusive tmin the composited sequence, and therefore the image, is the
-// same (rejected crossings only ever advanced `last`), while far fewer rounds are needed.
+// same (rejected crossings only ever advanced `last`), while far fewer rounds are needed.  FAST
+// also evaluates the response before the clip: an accepted crossing has its line within kS of
+// the centre in the kernel frame, i.e. inside the proxy's inscribed sphere, so a rejected proxy
+// needs no clip at all.
 #include "gvrt_internal.h"
 
 using namespace gvrt;
@@ -67,19 +71,55 @@ __device__ inline void kb_insert(float t, uint32_t id, float al, float (&kt)[K],
     }
 }
 
+// Insert two crossings of one proxy (a.t <= b.t, either may be INF_DIST) in one pass.  Per slot the
+// same strict-< rule as compareAndSwapHitPayloadValue (ties keep the earlier arrival first).
+template <int K>
+__device__ inline void kb_insert2(float ta, float tb, uint32_t id, float al, float (&kt)[K], uint32_t (&kid)[K],
+                                  float (&ka)[K]) {
+    float pt0 = ta, pt1 = tb;
+    uint32_t pi0 = id, pi1 = id;
+    float pa0 = al, pa1 = al;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const bool c0 = pt0 < kt[i];
+        const float st = kt[i];
+        const uint32_t si = kid[i];
+        const float sa = ka[i];
+        kt[i] = c0 ? pt0 : st;
+        kid[i] = c0 ? pi0 : si;
+        ka[i] = c0 ? pa0 : sa;
+        const float xt = c0 ? st : pt0;  // displaced (larger) of slot / pending 0
+        const uint32_t xi = c0 ? si : pi0;
+        const float xa = c0 ? sa : pa0;
+        const bool c1 = pt1 < xt;
+        pt0 = c1 ? pt1 : xt;
+        pi0 = c1 ? pi1 : xi;
+        pa0 = c1 ? pa1 : xa;
+        pt1 = c1 ? xt : pt1;
+        pi1 = c1 ? xi : pi1;
+        pa1 = c1 ? xa : pa1;
+    }
+}
+
 __device__ inline uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ inline float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 
-template <bool LITERAL, bool ADAPTIVE>
-__global__ __launch_bounds__(256) void k_render(RenderArgs a) {
+template <bool LITERAL, bool ADAPTIVE, int KB>
+__global__ __launch_bounds__(256) void k_render(const RenderArgs a, const Bvh4Node* __restrict__ nodes_,
+                                                const RenderRec* __restrict__ recs_, const float* __restrict__ sh_,
+                                                const float* __restrict__ view_inv_, const uint32_t* __restrict__ tiles_,
+                                                uint8_t* __restrict__ rgba8_, float* __restrict__ rgba32f_,
+                                                float* __restrict__ ray_dirs_, uint32_t* __restrict__ hit_counts_,
+                                                unsigned long long* __restrict__ stats_) {
     __shared__ int32_t s_stack[4][STACK_DEPTH];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const uint64_t tile_idx = (uint64_t)blockIdx.x * 4 + wid;
     if (tile_idx >= a.ntiles) return;  // wave-uniform
     uint32_t cam, tx, ty;
-    if (a.tiles) {
-        const uint32_t t = a.tiles[tile_idx];
+    if (tiles_) {
+        const uint32_t t = tiles_[tile_idx];
         cam = t >> 24;
         ty = (t >> 12) & 0xFFFu;
         tx = t & 0xFFFu;
@@ -95,7 +135,7 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
     const bool valid = px < a.width && py < a.height && cam < a.ncams;
 
     // ---- ray generation (particleRendering.comp:123-129, raygen.rgen:116-121)
-    const float* V = a.view_inv + 16 * (cam < a.ncams ? cam : 0);
+    const float* V = view_inv_ + 16 * (cam < a.ncams ? cam : 0);
     const float u = ((float)px + a.pixel_offset) / (float)a.width;
     const float v = ((float)py + a.pixel_offset) / (float)a.height;
     const float nx = u * 2.0f - 1.0f, ny = v * 2.0f - 1.0f;
@@ -115,31 +155,6 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
     const float dzs = fabsf(d.z) < 1e-12f ? copysignf(1e-12f, d.z) : d.z;
     const f3 inv = mk3(1.0f / dxs, 1.0f / dys, 1.0f / dzs);
 
-    // SH basis of the ray direction: the scalar factors of radianceFromSpH
-    // (gaussianfunctions.glsl:122-151), signs folded, zero past sph_eval_degree.
-    float shb[16];
-    {
-        const float x = d.x, y = d.y, z = d.z;
-        const uint32_t deg = a.sph_deg;
-        shb[0] = SH_C0;
-        const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-        shb[1] = deg > 0 ? -(SH_C1 * y) : 0.f;
-        shb[2] = deg > 0 ? SH_C1 * z : 0.f;
-        shb[3] = deg > 0 ? -(SH_C1 * x) : 0.f;
-        shb[4] = deg > 1 ? SH_C2_0 * xy : 0.f;
-        shb[5] = deg > 1 ? SH_C2_1 * yz : 0.f;
-        shb[6] = deg > 1 ? SH_C2_2 * (2.0f * zz - xx - yy) : 0.f;
-        shb[7] = deg > 1 ? SH_C2_3 * xz : 0.f;
-        shb[8] = deg > 1 ? SH_C2_4 * (xx - yy) : 0.f;
-        shb[9] = deg > 2 ? SH_C3_0 * y * (3.0f * xx - yy) : 0.f;
-        shb[10] = deg > 2 ? SH_C3_1 * xy * z : 0.f;
-        shb[11] = deg > 2 ? SH_C3_2 * y * (4.0f * zz - xx - yy) : 0.f;
-        shb[12] = deg > 2 ? SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) : 0.f;
-        shb[13] = deg > 2 ? SH_C3_4 * x * (4.0f * zz - xx - yy) : 0.f;
-        shb[14] = deg > 2 ? SH_C3_5 * z * (xx - yy) : 0.f;
-        shb[15] = deg > 2 ? SH_C3_6 * x * (xx - 3.0f * yy) : 0.f;
-    }
-
     // intersectAABB (gaussianfunctions.glsl:8-16, Q12)
     float tminb, tmaxb;
     {
@@ -152,11 +167,12 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
     float last = fmaxf(0.0f, tminb - EPS_T);
     float T = 1.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f, calpha = a.alpha_init;
     uint32_t nacc = 0, nproc = 0, rounds = 0;
+    uint32_t w_nodes = 0, w_leaves = 0, l_leaves = 0;  // wave node visits, wave leaf visits, lane leaf tests
     bool active = valid && a.nrecs > 0 && (last <= tmaxb) && (T > a.min_transmittance);
 
-    float kt[K_HITS];
-    uint32_t kid[K_HITS];
-    float ka[K_HITS];
+    float kt[KB];
+    uint32_t kid[KB];
+    float ka[KB];
     int32_t* stack = s_stack[wid];
 
     while (__ballot(active)) {
@@ -165,104 +181,151 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
         const float tlo = last + EPS_T;
         const float thi = tmaxb + EPS_T;
 #pragma unroll
-        for (int i = 0; i < K_HITS; ++i) {
+        for (int i = 0; i < KB; ++i) {
             kt[i] = INF_DIST;
             kid[i] = INVALID_ID;
-            ka[i] = 0.0f;
+            ka[i] = 0.0f;  // never read for an empty slot, but keeps the register set defined
         }
 
-        // ---------------- trace(): packet traversal of the LBVH
+        // ---------------- trace(): packet traversal of the 4-wide LBVH
         int sp = 0;
         int32_t node = 0;
         while (true) {
-            const BvhNode nd = a.nodes[node];
-            const float tc = fminf(thi, kt[K_HITS - 1]);
-            float e0, e1;
-            const bool h0 = active && box_hit(nd.l0x, nd.l0y, nd.l0z, nd.h0x, nd.h0y, nd.h0z, o, inv, tlo, tc, e0);
-            const bool h1 = active && box_hit(nd.l1x, nd.l1y, nd.l1z, nd.h1x, nd.h1y, nd.h1z, o, inv, tlo, tc, e1);
-            uint64_t b0 = __ballot(h0), b1 = __ballot(h1);
-            const int32_t c0 = unii(nd.c0), c1 = unii(nd.c1);
+            const Bvh4Node nd = nodes_[node];  // whole node, unconditionally: 2x s_load_dwordx16
+            ++w_nodes;
+            const float tc = fminf(thi, kt[KB - 1]);
+            bool hit[4];
+            float ent[4];
+            uint64_t bal[4];
 #pragma unroll
-            for (int side = 0; side < 2; ++side) {
-                const int32_t cc = side ? c1 : c0;
-                const uint64_t bb = side ? b1 : b0;
-                const bool hh = side ? h1 : h0;
-                if (bb && cc < 0 && !(side == 1 && a.root_is_leaf)) {
-                    const uint32_t gi = uni((uint32_t)(~cc));
-                    if (hh) {
-                        // ---- leaf: analytic icosahedron clip + response (processHit's math)
-                        const RenderRec rec = a.recs[gi];
+            for (int k = 0; k < 4; ++k) {
+                hit[k] = box_hit(nd.lox[k], nd.loy[k], nd.loz[k], nd.hix[k], nd.hiy[k], nd.hiz[k], o, inv, tlo, tc,
+                                 ent[k]) &&
+                         active;
+                bal[k] = __ballot(hit[k]);
+            }
+            int32_t ch[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ch[k] = unii(nd.child[k]);
+            // leaves first (the k-buffer orders them); one rolled loop = one k-buffer insertion site
+            uint32_t leafmask = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (bal[k] && ch[k] < 0) {
+                    leafmask |= 1u << k;
+                }
+            }
+            leafmask = uni(leafmask);
+            const uint32_t leaves_here = leafmask;
+#pragma unroll 1
+            while (leafmask) {
+                const int k = __builtin_ctz(leafmask);
+                leafmask &= leafmask - 1;
+                const uint64_t bk = k == 0 ? bal[0] : (k == 1 ? bal[1] : (k == 2 ? bal[2] : bal[3]));
+                const int32_t ck = k == 0 ? ch[0] : (k == 1 ? ch[1] : (k == 2 ? ch[2] : ch[3]));
+                {
+                    const uint32_t gi = uni((uint32_t)(~ck));
+                    ++w_leaves;
+                    const RenderRec rec = recs_[gi];  // whole record, before the lane branch: s_load_dwordx16
+                    if ((bk >> lane) & 1ull) {
+                        ++l_leaves;
+                        // ---- leaf: response (processHit's math) + analytic icosahedron clip
+                        const float isx = rec.isx, isy = rec.isy, isz = rec.isz;
                         const f3 dxo = o - mk3(rec.px, rec.py, rec.pz);
-                        const f3 ok = mk3(rec.c0x * dxo.x + rec.c1x * dxo.y + rec.c2x * dxo.z,
-                                          rec.c0y * dxo.x + rec.c1y * dxo.y + rec.c2y * dxo.z,
-                                          rec.c0z * dxo.x + rec.c1z * dxo.y + rec.c2z * dxo.z) *
-                                      mk3(rec.isx, rec.isy, rec.isz);
-                        const f3 dk = mk3(rec.c0x * d.x + rec.c1x * d.y + rec.c2x * d.z,
-                                          rec.c0y * d.x + rec.c1y * d.y + rec.c2y * d.z,
-                                          rec.c0z * d.x + rec.c1z * d.y + rec.c2z * d.z) *
-                                      mk3(rec.isx, rec.isy, rec.isz);
-                        const float hk =
-                            ADAPTIVE ? kernel_scale(rec.density, a.kmin, a.kopts, a.kdeg) * SQRT3 : a.kernel_h;
-                        float tn = -INFINITY, tf = INFINITY;
+                        const f3 ok = mk3((rec.c0x * dxo.x + rec.c1x * dxo.y + rec.c2x * dxo.z) * isx,
+                                          (rec.c0y * dxo.x + rec.c1y * dxo.y + rec.c2y * dxo.z) * isy,
+                                          (rec.c0z * dxo.x + rec.c1z * dxo.y + rec.c2z * dxo.z) * isz);
+                        const f3 dk = mk3((rec.c0x * d.x + rec.c1x * d.y + rec.c2x * d.z) * isx,
+                                          (rec.c0y * d.x + rec.c1y * d.y + rec.c2y * d.z) * isy,
+                                          (rec.c0z * d.x + rec.c1z * d.y + rec.c2z * d.z) * isz);
+                        // particleResponse / alpha (gaussianfunctions.glsl:186-200)
+                        const float l2 = dk.x * dk.x + dk.y * dk.y + dk.z * dk.z;
+                        const f3 grd = l2 > 0.0f ? dk * (1.0f / sqrtf(l2)) : dk;
+                        const f3 gc = cross3(grd, ok);
+                        const float gd = gc.x * gc.x + gc.y * gc.y + gc.z * gc.z;
+                        const float gres = expf(KERNEL_S * gd * gd);
+                        const float galpha = fminf(0.99f, gres * rec.density);
+                        const bool acc = (gres > a.min_response) && (galpha > a.alpha_min);
+                        if (LITERAL || acc) {
+                            const float hk =
+                                ADAPTIVE ? kernel_scale(rec.density, a.kmin, a.kopts, a.kdeg) * SQRT3 : a.kernel_h;
+                            float tn = -INFINITY, tf = INFINITY;
 #define GVRT_SLAB(AX, AY, AZ)                                      \
     {                                                              \
         const float sa = (AX) * ok.x + (AY) * ok.y + (AZ) * ok.z;  \
         const float sb = (AX) * dk.x + (AY) * dk.y + (AZ) * dk.z;  \
-        const float ib = 1.0f / sb;                                \
+        const float ib = __builtin_amdgcn_rcpf(sb);                \
         const float t1 = (-hk - sa) * ib, t2 = (hk - sa) * ib;     \
         tn = fmaxf(tn, fminf(t1, t2));                             \
         tf = fminf(tf, fmaxf(t1, t2));                             \
     }
-                        GVRT_SLAB(1.f, 1.f, 1.f)
-                        GVRT_SLAB(1.f, 1.f, -1.f)
-                        GVRT_SLAB(1.f, -1.f, 1.f)
-                        GVRT_SLAB(-1.f, 1.f, 1.f)
-                        GVRT_SLAB(0.f, PHI, IPHI)
-                        GVRT_SLAB(0.f, PHI, -IPHI)
-                        GVRT_SLAB(IPHI, 0.f, PHI)
-                        GVRT_SLAB(-IPHI, 0.f, PHI)
-                        GVRT_SLAB(PHI, IPHI, 0.f)
-                        GVRT_SLAB(PHI, -IPHI, 0.f)
+                            GVRT_SLAB(1.f, 1.f, 1.f)
+                            GVRT_SLAB(1.f, 1.f, -1.f)
+                            GVRT_SLAB(1.f, -1.f, 1.f)
+                            GVRT_SLAB(-1.f, 1.f, 1.f)
+                            GVRT_SLAB(0.f, PHI, IPHI)
+                            GVRT_SLAB(0.f, PHI, -IPHI)
+                            GVRT_SLAB(IPHI, 0.f, PHI)
+                            GVRT_SLAB(-IPHI, 0.f, PHI)
+                            GVRT_SLAB(PHI, IPHI, 0.f)
+                            GVRT_SLAB(PHI, -IPHI, 0.f)
 #undef GVRT_SLAB
-                        if (tn <= tf) {
-                            // particleResponse / alpha (gaussianfunctions.glsl:186-200)
-                            const float l2 = dk.x * dk.x + dk.y * dk.y + dk.z * dk.z;
-                            const f3 grd = l2 > 0.0f ? dk * (1.0f / sqrtf(l2)) : dk;
-                            const f3 gc = cross3(grd, ok);
-                            const float gd = gc.x * gc.x + gc.y * gc.y + gc.z * gc.z;
-                            const float gres = expf(KERNEL_S * gd * gd);
-                            const float galpha = fminf(0.99f, gres * rec.density);
-                            const bool acc = (gres > a.min_response) && (galpha > a.alpha_min);
-                            if (LITERAL || acc) {
+                            if (tn <= tf) {
                                 const float al = acc ? galpha : -1.0f;
                                 const bool in0 = (a.tmin_inclusive ? tn >= tlo : tn > tlo) && tn <= thi;
                                 const bool in1 = (a.tmin_inclusive ? tf >= tlo : tf > tlo) && tf <= thi;
-                                if (in0) kb_insert<K_HITS>(tn, gi, al, kt, kid, ka);
-                                if (in1) kb_insert<K_HITS>(tf, gi, al, kt, kid, ka);
+                                const float ta = in0 ? tn : (in1 ? tf : INF_DIST);
+                                const float tb = (in0 && in1) ? tf : INF_DIST;
+                                if (ta < kt[KB - 1]) kb_insert2<KB>(ta, tb, gi, al, kt, kid, ka);
                             }
                         }
                     }
-                    if (side == 0) b0 = 0;
-                    else b1 = 0;
                 }
             }
-            if (b0 && b1) {
-                const uint64_t both = __ballot(h0 && h1);
-                const uint64_t pref0 = __ballot(h0 && h1 && e0 <= e1);
-                const bool first0 = 2 * __popcll(pref0) >= __popcll(both);
-                const int32_t near = first0 ? c0 : c1, far = first0 ? c1 : c0;
-                stack[sp] = far;
-                ++sp;
-                node = near;
-            } else if (b0) {
-                node = c0;
-            } else if (b1) {
-                node = c1;
-            } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if ((leaves_here >> k) & 1u) bal[k] = 0;
+            // internal children: nearest first (entry distance of the first lane that hits each)
+            float key[4];
+            int32_t cid[4];
+            int nint = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                key[k] = INFINITY;
+                cid[k] = -1;
+                if (bal[k]) {
+                    const int first = __builtin_ctzll(bal[k]);
+                    key[k] = __shfl(ent[k], first);
+                    cid[k] = ch[k];
+                    ++nint;
+                }
+            }
+            if (nint == 0) {
                 if (sp == 0) break;
                 --sp;
                 node = unii(stack[sp]);
+                continue;
             }
+            // sort the (key, child) pairs ascending: 5-comparator network on uniform values
+#define GVRT_CX(i, j)                                   \
+    {                                                   \
+        if (key[j] < key[i]) {                          \
+            const float tk = key[i];                    \
+            key[i] = key[j];                            \
+            key[j] = tk;                                \
+            const int32_t tc2 = cid[i];                 \
+            cid[i] = cid[j];                            \
+            cid[j] = tc2;                               \
+        }                                               \
+    }
+            GVRT_CX(0, 1) GVRT_CX(2, 3) GVRT_CX(0, 2) GVRT_CX(1, 3) GVRT_CX(1, 2)
+#undef GVRT_CX
+            // cid[0..nint-1] are the hit internal children, nearest first
+            for (int k = nint - 1; k >= 1; --k) {
+                stack[sp] = cid[k];
+                ++sp;
+            }
+            node = unii(cid[0]);
         }
 
         // ---------------- process k hits (particleRendering.comp:153-187)
@@ -270,23 +333,53 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
             if (kid[0] == INVALID_ID) {
                 active = false;
             } else {
-#pragma unroll
-                for (int i = 0; i < K_HITS; ++i) {
-                    if (kid[i] != INVALID_ID && T > a.min_transmittance) {
+                // rolled loop over slots: composite slot 0, then shift the buffer down by one
+#pragma unroll 1
+                for (int it = 0; it < KB; ++it) {
+                    if (kid[0] != INVALID_ID && T > a.min_transmittance) {
                         ++nproc;
-                        if (ka[i] > 0.0f) {
-                            const float weight = ka[i] * T;
-                            const float4* s4 = reinterpret_cast<const float4*>(a.sh + 48ull * kid[i]);
+                        if (ka[0] > 0.0f) {
+                            const float weight = ka[0] * T;
+                            const float4* s4 = reinterpret_cast<const float4*>(sh_ + 48ull * kid[0]);
                             float rr = 0.f, rg = 0.f, rb = 0.f;
-                            // 16 coefficients x rgb = 12 float4
-#pragma unroll
+                            // 16 coefficients x rgb = 12 float4, in 4 rolled chunks of 3 (few live VGPRs)
+#pragma unroll 1
                             for (int q = 0; q < 4; ++q) {
                                 const float4 v0 = s4[3 * q], v1 = s4[3 * q + 1], v2 = s4[3 * q + 2];
+                                // basis factors 4q..4q+3 of radianceFromSpH (gaussianfunctions.glsl:122-151),
+                                // signs folded, zero past sph_eval_degree; recomputed per chunk so they
+                                // are not held in registers through the traversal
+                                float x = d.x, y = d.y, z = d.z;
+                                asm volatile("" : "+v"(x), "+v"(y), "+v"(z));  // keep LICM from hoisting 16 factors
+                                const uint32_t deg = a.sph_deg;
+                                const float xx = x * x, yy = y * y, zz = z * z;
+                                float b0, b1, b2, b3;
+                                if (q == 0) {
+                                    b0 = SH_C0;
+                                    b1 = deg > 0 ? -(SH_C1 * y) : 0.f;
+                                    b2 = deg > 0 ? SH_C1 * z : 0.f;
+                                    b3 = deg > 0 ? -(SH_C1 * x) : 0.f;
+                                } else if (q == 1) {
+                                    b0 = deg > 1 ? SH_C2_0 * (x * y) : 0.f;
+                                    b1 = deg > 1 ? SH_C2_1 * (y * z) : 0.f;
+                                    b2 = deg > 1 ? SH_C2_2 * (2.0f * zz - xx - yy) : 0.f;
+                                    b3 = deg > 1 ? SH_C2_3 * (x * z) : 0.f;
+                                } else if (q == 2) {
+                                    b0 = deg > 1 ? SH_C2_4 * (xx - yy) : 0.f;
+                                    b1 = deg > 2 ? SH_C3_0 * y * (3.0f * xx - yy) : 0.f;
+                                    b2 = deg > 2 ? SH_C3_1 * (x * y) * z : 0.f;
+                                    b3 = deg > 2 ? SH_C3_2 * y * (4.0f * zz - xx - yy) : 0.f;
+                                } else {
+                                    b0 = deg > 2 ? SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) : 0.f;
+                                    b1 = deg > 2 ? SH_C3_4 * x * (4.0f * zz - xx - yy) : 0.f;
+                                    b2 = deg > 2 ? SH_C3_5 * z * (xx - yy) : 0.f;
+                                    b3 = deg > 2 ? SH_C3_6 * x * (xx - 3.0f * yy) : 0.f;
+                                }
                                 // coefficients 4q..4q+3: (v0.xyz) (v0.w v1.xy) (v1.zw v2.x) (v2.yzw)
-                                rr += shb[4 * q] * v0.x; rg += shb[4 * q] * v0.y; rb += shb[4 * q] * v0.z;
-                                rr += shb[4 * q + 1] * v0.w; rg += shb[4 * q + 1] * v1.x; rb += shb[4 * q + 1] * v1.y;
-                                rr += shb[4 * q + 2] * v1.z; rg += shb[4 * q + 2] * v1.w; rb += shb[4 * q + 2] * v2.x;
-                                rr += shb[4 * q + 3] * v2.y; rg += shb[4 * q + 3] * v2.z; rb += shb[4 * q + 3] * v2.w;
+                                rr += b0 * v0.x; rg += b0 * v0.y; rb += b0 * v0.z;
+                                rr += b1 * v0.w; rg += b1 * v1.x; rb += b1 * v1.y;
+                                rr += b2 * v1.z; rg += b2 * v1.w; rb += b2 * v2.x;
+                                rr += b3 * v2.y; rg += b3 * v2.z; rb += b3 * v2.w;
                             }
                             rr = fmaxf(rr + 0.5f, 0.0f);
                             rg = fmaxf(rg + 0.5f, 0.0f);
@@ -295,11 +388,18 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
                             cg += rg * weight;
                             cb += rb * weight;
                             calpha += 1.0f;
-                            T *= (1.0f - ka[i]);
+                            T *= (1.0f - ka[0]);
                             ++nacc;
                         }
-                        last = fmaxf(last, kt[i]);
+                        last = fmaxf(last, kt[0]);
                     }
+#pragma unroll
+                    for (int i = 0; i < KB - 1; ++i) {
+                        kt[i] = kt[i + 1];
+                        kid[i] = kid[i + 1];
+                        ka[i] = ka[i + 1];
+                    }
+                    kid[KB - 1] = INVALID_ID;
                 }
                 active = (last <= tmaxb) && (T > a.min_transmittance);
             }
@@ -310,35 +410,39 @@ __global__ __launch_bounds__(256) void k_render(RenderArgs a) {
     if (valid) {
         const uint64_t pix = ((uint64_t)cam * a.height + py) * a.width + px;
         const uint64_t oi = a.packed ? tile_idx * 64 + lane : pix;
-        if (a.rgba32f) reinterpret_cast<float4*>(a.rgba32f)[oi] = make_float4(cr, cg, cb, calpha);
-        if (a.rgba8) {
+        if (rgba32f_) reinterpret_cast<float4*>(rgba32f_)[oi] = make_float4(cr, cg, cb, calpha);
+        if (rgba8_) {
             auto q8 = [](float f) -> uint32_t { return (uint32_t)(fminf(fmaxf(f, 0.0f), 1.0f) * 255.0f + 0.5f); };
-            reinterpret_cast<uint32_t*>(a.rgba8)[oi] = q8(cr) | (q8(cg) << 8) | (q8(cb) << 16) | (q8(calpha) << 24);
+            reinterpret_cast<uint32_t*>(rgba8_)[oi] = q8(cr) | (q8(cg) << 8) | (q8(cb) << 16) | (q8(calpha) << 24);
         }
-        if (a.hit_counts) a.hit_counts[oi] = nacc;
-        if (a.ray_dirs) {
+        if (hit_counts_) hit_counts_[oi] = nacc;
+        if (ray_dirs_) {
             const uint64_t di = a.ray_dirs_layout == 1
                                     ? ((uint64_t)cam * a.width * a.height + (uint64_t)px * a.height + py)
                                     : pix;
-            reinterpret_cast<float4*>(a.ray_dirs)[di] = make_float4(d.x, d.y, d.z, 0.0f);
+            reinterpret_cast<float4*>(ray_dirs_)[di] = make_float4(d.x, d.y, d.z, 0.0f);
         }
     } else if (a.packed) {
         const uint64_t oi = tile_idx * 64 + lane;
-        if (a.rgba32f) reinterpret_cast<float4*>(a.rgba32f)[oi] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (a.rgba8) reinterpret_cast<uint32_t*>(a.rgba8)[oi] = 0u;
-        if (a.hit_counts) a.hit_counts[oi] = 0u;
+        if (rgba32f_) reinterpret_cast<float4*>(rgba32f_)[oi] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (rgba8_) reinterpret_cast<uint32_t*>(rgba8_)[oi] = 0u;
+        if (hit_counts_) hit_counts_[oi] = 0u;
     }
-    if (a.stats) {
-        unsigned long long s0 = nproc, s1 = nacc, s2 = rounds;
+    if (stats_) {
+        unsigned long long s0 = nproc, s1 = nacc, s2 = rounds, s5 = l_leaves;
         for (int off = 32; off > 0; off >>= 1) {
             s0 += __shfl_xor(s0, off);
             s1 += __shfl_xor(s1, off);
             s2 += __shfl_xor(s2, off);
+            s5 += __shfl_xor(s5, off);
         }
         if (lane == 0) {
-            atomicAdd(a.stats + 0, s0);
-            atomicAdd(a.stats + 1, s1);
-            atomicAdd(a.stats + 2, s2);
+            atomicAdd(stats_ + 0, s0);
+            atomicAdd(stats_ + 1, s1);
+            atomicAdd(stats_ + 2, s2);
+            atomicAdd(stats_ + 3, (unsigned long long)w_nodes);
+            atomicAdd(stats_ + 4, (unsigned long long)w_leaves);
+            atomicAdd(stats_ + 5, s5);
         }
     }
 }
@@ -361,13 +465,25 @@ __global__ __launch_bounds__(256) void k_unpack(const uint32_t* __restrict__ pac
 gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64_t nwaves, bool literal) {
     const uint64_t blocks = (nwaves + 3) / 4;
     if (blocks == 0) return GVRT_OK;
+    if (blocks > 0x7FFFFFFFull) return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "too many tiles");
     const bool adaptive = (a.kopts & 1u) != 0;
-    if (literal) {
-        if (adaptive) hipLaunchKernelGGL((k_render<true, true>), dim3((unsigned)blocks), dim3(256), 0, c->stream, a);
-        else hipLaunchKernelGGL((k_render<true, false>), dim3((unsigned)blocks), dim3(256), 0, c->stream, a);
+    const dim3 g((unsigned)blocks), b(256);
+    // every pointer is its own __restrict__ argument: the uniform node / record loads can then be
+    // proven unclobbered by the output stores and are emitted as scalar (s_load) loads
+#define KARGS a.nodes, a.recs, a.sh, a.view_inv, a.tiles, a.rgba8, a.rgba32f, a.ray_dirs, a.hit_counts, a.stats
+    if (literal) {  // the reference's 16-slot k-buffer (MAX_HIT_PER_TRACE)
+        if (adaptive) hipLaunchKernelGGL((k_render<true, true, K_HITS>), g, b, 0, c->stream, a, KARGS);
+        else hipLaunchKernelGGL((k_render<true, false, K_HITS>), g, b, 0, c->stream, a, KARGS);
+    } else if (adaptive) {
+        hipLaunchKernelGGL((k_render<false, true, K_HITS>), g, b, 0, c->stream, a, KARGS);
     } else {
-        if (adaptive) hipLaunchKernelGGL((k_render<false, true>), dim3((unsigned)blocks), dim3(256), 0, c->stream, a);
-        else hipLaunchKernelGGL((k_render<false, false>), dim3((unsigned)blocks), dim3(256), 0, c->stream, a);
+        // FAST: the k-buffer depth only sets the number of traversal rounds, not the image
+        switch (a.kfast) {
+            case 8: hipLaunchKernelGGL((k_render<false, false, 8>), g, b, 0, c->stream, a, KARGS); break;
+            case 12: hipLaunchKernelGGL((k_render<false, false, 12>), g, b, 0, c->stream, a, KARGS); break;
+            case 24: hipLaunchKernelGGL((k_render<false, false, 24>), g, b, 0, c->stream, a, KARGS); break;
+            default: hipLaunchKernelGGL((k_render<false, false, K_HITS>), g, b, 0, c->stream, a, KARGS); break;
+        }
     }
     GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;

@@ -70,7 +70,9 @@ typedef struct {
     uint32_t mode;                   /* GVRT_MODE_FAST (default) or GVRT_MODE_LITERAL */
     uint32_t max_rounds;             /* 0 = unlimited */
     uint32_t ray_dirs_layout;        /* 0: [cam][y][x]; 1: light-field [cam][x][y] (raygenGaussianLightField.rgen:129) */
-    uint32_t reserved[5];
+    uint32_t kbuffer_depth;          /* FAST only: 0 = default (16); 8, 12, 16 or 24 slots per ray (sets
+                                        the number of traversal rounds, not the image) */
+    uint32_t reserved[4];
 } gvrt_render_params;
 
 #define GVRT_MODE_FAST 0u    /* only accepted crossings enter the k-buffer (same image) */
@@ -108,6 +110,9 @@ typedef struct {
     float render_ms;       /* device time of the last render kernel (HIP events on the handle's stream) */
     float pad1;
     uint64_t device_bytes; /* bytes of device memory held by the handle */
+    uint64_t wave_node_visits;  /* traversal diagnostics of the last render (stats enabled): */
+    uint64_t wave_leaf_visits;  /*   BVH nodes / leaves visited per wave, summed over waves,  */
+    uint64_t lane_leaf_tests;   /*   and ray-proxy clip tests summed over lanes               */
 } gvrt_stats;
 
 /* --------------------------------------------------------------------------------------- */

@@ -1,0 +1,41 @@
+"""Traversal diagnostics of the render kernel on a bench scene (stats-enabled renders).
+
+python scripts/diag_traversal.py [config] [kbuffer depths...]
+"""
+import importlib
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+gv = importlib.import_module("3dgvrt_lightfield_amd")
+cfg = sys.argv[1] if len(sys.argv) > 1 else "bicycle"
+depths = [int(x) for x in sys.argv[2:]] or [16]
+gen, W, H, _ = gv.scene.CONFIGS[cfg]
+s = gv.scene.make(**gen)
+vi, pi = (gv.scene.mipnerf_camera(W, H) if cfg != "config1" else gv.scene.config1_camera(W, H))
+waves = (W + 7) // 8 * ((H + 7) // 8)
+rays = W * H
+out = {}
+with gv.Renderer(0) as r:
+    r.prepare(s)
+    runs = [("literal", gv.MODE_LITERAL, 0)] + [(f"fast_k{k}", gv.MODE_FAST, k) for k in depths]
+    for name, mode, k in runs:
+        kw = dict(mode=mode, kbuffer_depth=k, rgba8=False, rgba32f=False)
+        r.render(vi, pi, W, H, **kw)  # warm
+        r.set_stats(True)
+        r.render(vi, pi, W, H, **kw)
+        st = r.stats()
+        r.set_stats(False)
+        ms = []
+        for _ in range(5):
+            r.render(vi, pi, W, H, **kw)
+            ms.append(r.stats()["render_ms"])
+        ms = sorted(ms)[len(ms) // 2]
+        out[name] = {"ms": round(ms, 3), "Mrays/s": round(rays / ms / 1e3, 1),
+                     "crossings/ray": round(st["crossings"] / rays, 3),
+                     "accepted/ray": round(st["accepted"] / rays, 3), "rounds/ray": round(st["rounds"] / rays, 3),
+                     "node_visits/wave": round(st["wave_node_visits"] / waves, 1),
+                     "leaf_visits/wave": round(st["wave_leaf_visits"] / waves, 1),
+                     "lane_leaf_tests/ray": round(st["lane_leaf_tests"] / rays, 2), "bvh_depth": st["bvh_depth"]}
+print(json.dumps(out, indent=1))

@@ -1,0 +1,15 @@
+"""Minimal driver for rocprofv3: builds the bench scene and renders the bench view N times."""
+import importlib, os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+gv = importlib.import_module("3dgvrt_lightfield_amd")
+cfg = os.environ.get("GVRT_CFG", "bicycle")
+n = int(os.environ.get("GVRT_N", "5"))
+k = int(os.environ.get("GVRT_K", "0"))
+gen, W, H, _ = gv.scene.CONFIGS[cfg]
+s = gv.scene.make(**gen)
+vi, pi = (gv.scene.mipnerf_camera(W, H) if cfg != "config1" else gv.scene.config1_camera(W, H))
+with gv.Renderer(0) as r:
+    r.prepare(s)
+    for _ in range(n):
+        r.render(vi, pi, W, H, kbuffer_depth=k, rgba8=False, rgba32f=False)
+    print("render_ms", r.stats()["render_ms"])
