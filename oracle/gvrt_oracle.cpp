@@ -378,9 +378,20 @@ inline bool rayTri(V3 org, V3 dir, int kx, int ky, int kz, float Sx, float Sy, f
         V = (float)((double)Ax * Cy - (double)Ay * Cx);
         W = (float)((double)Bx * Ay - (double)By * Ax);
     }
-    if ((U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f)) return false;
     const float det = U + V + W;
     if (det == 0.0f) return false;
+    // Shared-edge ownership: a ray exactly on an edge must hit one of the two triangles sharing it,
+    // not both (watertight hardware semantics).  The sign given to a zero edge function is
+    // antisymmetric in the edge direction, and a consistently wound mesh traverses a shared edge in
+    // opposite directions, so exactly one triangle owns it.
+    auto own = [](float e, float ex, float ey) -> float {
+        if (e != 0.0f) return e;
+        return (ey > 0.0f || (ey == 0.0f && ex > 0.0f)) ? 1.0f : -1.0f;
+    };
+    const float Us = own(U, Cx - Bx, Cy - By);  // edge B->C
+    const float Vs = own(V, Ax - Cx, Ay - Cy);  // edge C->A
+    const float Ws = own(W, Bx - Ax, By - Ay);  // edge A->B
+    if ((Us < 0.0f || Vs < 0.0f || Ws < 0.0f) && (Us > 0.0f || Vs > 0.0f || Ws > 0.0f)) return false;
     const float Az = Sz * comp(A, kz), Bz = Sz * comp(B, kz), Cz = Sz * comp(C, kz);
     const float T = U * Az + V * Bz + W * Cz;
     tOut = T / det;

@@ -134,8 +134,10 @@ def render(enc, view_inv, proj_inv, width, height, ncams=1, params=None, subset=
 def eval_response(density_rec, o, d):
     g = np.zeros(1, np.float32)
     a = np.zeros(1, np.float32)
-    lib().oracle_eval_response(_p(np.ascontiguousarray(density_rec, np.float32)), _p(np.asarray(o, np.float32)),
-                               _p(np.asarray(d, np.float32)), _p(g), _p(a))
+    rec = np.ascontiguousarray(density_rec, np.float32)
+    oo = np.ascontiguousarray(o, np.float32)
+    dd = np.ascontiguousarray(d, np.float32)
+    lib().oracle_eval_response(_p(rec), _p(oo), _p(dd), _p(g), _p(a))
     return float(g[0]), float(a[0])
 
 
@@ -145,8 +147,9 @@ def kernel_scale(density, min_response=0.0113, opts=0, degree=4.0):
 
 def radiance_from_sh(deg, sh48, d):
     out = np.zeros(3, np.float32)
-    lib().oracle_radiance_from_sh(deg, _p(np.ascontiguousarray(sh48, np.float32)), _p(np.asarray(d, np.float32)),
-                                  _p(out))
+    c = np.ascontiguousarray(sh48, np.float32)
+    dd = np.ascontiguousarray(d, np.float32)
+    lib().oracle_radiance_from_sh(deg, _p(c), _p(dd), _p(out))
     return out
 
 

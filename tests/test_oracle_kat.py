@@ -1,0 +1,237 @@
+"""CPU oracle: known-answer tests and golden vectors (no GPU).
+
+The oracle restates the reference GLSL (see oracle/gvrt_oracle.cpp).  No reference-produced vector
+exists for this path, so the oracle is pinned here by closed-form cases, by a second
+independent numpy restatement of the enclosing filter / SH evaluation, by the agreement of its
+literal 20-triangle mode with its analytic mode, and by committed golden fixtures.
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def one_gaussian(pos=(0, 0, 0), scale=0.2, opacity=0.5, fdc=(0.3, -0.2, 0.1), rot=(1, 0, 0, 0), frest=None):
+    return {"positions": np.asarray(pos, np.float32), "f_dc": np.asarray(fdc, np.float32),
+            "f_rest": np.zeros(45, np.float32) if frest is None else np.asarray(frest, np.float32),
+            "opacity": np.array([opacity], np.float32),
+            "scale": np.log(np.broadcast_to(np.asarray(scale, np.float32), (3,))).astype(np.float32),
+            "rotation": np.asarray(rot, np.float32)}
+
+
+def test_kernel_scale_constant(O):
+    # kernelScale(degree 4, 0.0113) = 2.997154714 (particlePrimitives.comp:98-104)
+    assert O.kernel_scale(0.7) == pytest.approx(2.997154714, rel=1e-6)
+    # closed form (ln(minResponse) / (-4.5/81))^(1/4)
+    assert O.kernel_scale(0.7) == pytest.approx((math.log(0.0113) / (-4.5 / 81)) ** 0.25, rel=1e-6)
+    # adaptive clamping: minResponse = min(0.0113 / density, 0.97)
+    d = 0.2
+    assert O.kernel_scale(d, opts=1) == pytest.approx((math.log(0.0113 / d) / (-4.5 / 81)) ** 0.25, rel=1e-5)
+
+
+def test_enclose_records_closed_form(O):
+    g = one_gaussian(pos=(0.1, -0.2, 0.3), scale=(0.1, 0.2, 0.3), opacity=1.5, rot=(2, 0, 0, 0))
+    g["scale"] = np.log(np.array([0.1, 0.2, 0.3], np.float32))
+    e = O.enclose(g)
+    assert e["m"] == 1
+    rec = e["density"]
+    np.testing.assert_array_equal(rec[:3], np.float32([0.1, -0.2, 0.3]))
+    assert rec[3] == pytest.approx(1 / (1 + math.exp(-1.5)), rel=1e-6)   # sigmoid
+    np.testing.assert_allclose(rec[4:8], [1, 0, 0, 0], atol=1e-7)          # normalized quaternion
+    np.testing.assert_allclose(rec[8:11], [0.1, 0.2, 0.3], rtol=1e-6)      # exp(scale)
+    assert rec[11] == 0.0
+    np.testing.assert_array_equal(e["sh"][:3], g["f_dc"])
+    # 12 vertices: identity rotation -> V_i * kS * scl * icosaVrtScale + pos
+    kS = O.kernel_scale(rec[3])
+    phi = 1.618033988749895
+    V = np.array([[-1, phi, 0], [1, phi, 0], [0, 1, -phi], [-phi, 0, -1], [-phi, 0, 1], [0, 1, phi], [phi, 0, 1],
+                  [0, -1, phi], [-1, -phi, 0], [0, -1, -phi], [phi, 0, -1], [1, -phi, 0]])
+    expect = V * (kS * np.array([0.1, 0.2, 0.3]) * 0.5 * 1.323169076499215) + [0.1, -0.2, 0.3]
+    np.testing.assert_allclose(e["verts"].reshape(12, 3), expect, rtol=1e-5, atol=1e-6)
+    # proxy inradius in the kernel frame is exactly kS: every face plane at distance kS
+    tri = e["tris"].reshape(20, 3)
+    vk = (e["verts"].reshape(12, 3) - [0.1, -0.2, 0.3]) / [0.1, 0.2, 0.3]
+    for a, b, c in tri:
+        n = np.cross(vk[b] - vk[a], vk[c] - vk[a])
+        n /= np.linalg.norm(n)
+        assert abs(np.dot(n, vk[a])) == pytest.approx(kS, rel=1e-5)
+
+
+def numpy_filter(s):
+    """Independent numpy restatement of particlePrimitives.comp:120-140 (Q5: neighbour reads, OOB = 0)."""
+    n = s["positions"].size // 3
+    fdc = s["f_dc"].reshape(n, 3).astype(np.float32)
+    spec = np.concatenate([s["f_rest"].astype(np.float32), np.zeros(135, np.float32)])
+    keep = []
+    for g in range(n):
+        if np.float32(np.sqrt(np.float32(np.sum(fdc[g] * fdc[g])))) > 3.0:
+            continue
+        acc = np.float32(0)
+        mx, mn = np.float32(0), np.float32(1e10)
+        for i in range(1, 45):
+            v = spec[45 * g + 3 * i: 45 * g + 3 * i + 3]
+            acc = np.float32(acc + np.float32(np.sqrt(np.float32(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]))))
+            mx, mn = max(mx, acc), min(mn, acc)
+        if mx / np.float32(mn + np.float32(1e-5)) > 150.0:
+            continue
+        keep.append(g)
+    return np.array(keep, np.uint32)
+
+
+def test_enclose_filter_vs_numpy(gv, O):
+    s = gv.scene.config1(n=400, seed=11)
+    e = O.enclose(s)
+    np.testing.assert_array_equal(e["src_index"], numpy_filter(s))
+    assert 0 < e["m"] < 400  # both filter cases fire on this seed
+
+
+def numpy_sh(deg, c, d):
+    """gaussianfunctions.glsl:122-151 in numpy (float64)."""
+    x, y, z = d
+    C0, C1 = 0.28209479177387814, 0.4886025119029199
+    C2 = [1.0925484305920792, -1.0925484305920792, 0.31539156525252005, -1.0925484305920792, 0.5462742152960396]
+    C3 = [-0.5900435899266435, 2.890611442640554, -0.4570457994644658, 0.3731763325901154, -0.4570457994644658,
+          1.445305721320277, -0.5900435899266435]
+    r = C0 * c[0]
+    if deg > 0:
+        r = r - C1 * y * c[1] + C1 * z * c[2] - C1 * x * c[3]
+    if deg > 1:
+        xx, yy, zz = x * x, y * y, z * z
+        r = r + C2[0] * x * y * c[4] + C2[1] * y * z * c[5] + C2[2] * (2 * zz - xx - yy) * c[6] + \
+            C2[3] * x * z * c[7] + C2[4] * (xx - yy) * c[8]
+    if deg > 2:
+        r = r + C3[0] * y * (3 * xx - yy) * c[9] + C3[1] * x * y * z * c[10] + C3[2] * y * (4 * zz - xx - yy) * c[11] + \
+            C3[3] * z * (2 * zz - 3 * xx - 3 * yy) * c[12] + C3[4] * x * (4 * zz - xx - yy) * c[13] + \
+            C3[5] * z * (xx - yy) * c[14] + C3[6] * x * (xx - 3 * yy) * c[15]
+    return np.maximum(r + 0.5, 0.0)
+
+
+@pytest.mark.parametrize("deg", [0, 1, 2, 3])
+def test_radiance_from_sh(O, deg):
+    rng = np.random.default_rng(deg)
+    for _ in range(20):
+        c = rng.normal(0, 0.5, (16, 3)).astype(np.float32)
+        d = rng.normal(size=3)
+        d = (d / np.linalg.norm(d)).astype(np.float32)
+        got = O.radiance_from_sh(deg, c.reshape(-1), d)
+        np.testing.assert_allclose(got, numpy_sh(deg, c.astype(np.float64), d.astype(np.float64)), rtol=1e-5,
+                                   atol=1e-6)
+
+
+def test_response_closed_form(O):
+    # isotropic unit Gaussian at the origin; a ray at perpendicular distance r: gres = exp(-r^4 / 18)
+    rec = np.array([0, 0, 0, 0.8, 1, 0, 0, 0, 1, 1, 1, 0], np.float32)
+    for r in (0.0, 0.5, 1.0, 2.0, 2.9, 3.1):
+        g, a = O.eval_response(rec, [r, 0.0, -5.0], [0.0, 0.0, 1.0])
+        assert g == pytest.approx(math.exp(-0.0555555555556 * r ** 4), rel=1e-5, abs=1e-12)
+        assert a == pytest.approx(min(0.99, g * 0.8), rel=1e-5, abs=1e-12)
+
+
+@pytest.mark.parametrize("proxy", [0, 1])
+def test_single_gaussian_two_crossings(gv, O, proxy):
+    g = one_gaussian()
+    e = O.enclose(g)
+    vi, pi = gv.camera.pinhole((0.0, 0.0, 3.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0, 1.0)
+    out = O.render(e, vi, pi, 2, 2, proxy_mode=proxy)
+    px = out["rgba32f"][0, 1, 1]  # offset 0: pixel (1,1) of a 2x2 image is the optical axis
+    a = min(0.99, 1 / (1 + math.exp(-0.5)))
+    c = np.maximum(0.28209479177387814 * np.array([0.3, -0.2, 0.1]) + 0.5, 0)
+    np.testing.assert_allclose(px[:3], c * a + c * a * (1 - a), rtol=1e-5)  # entry + exit face (Q1)
+    assert px[3] == 2.0                                                     # RQ alpha counts hits (Q10)
+    st = out["stats"][0, 1, 1]
+    assert st[0] == 2 and st[1] == 2
+    # a ray that misses everything: no crossing, zero radiance
+    assert (out["rgba32f"][0, 0, 0] == 0).all()
+
+
+def test_camera_inside_gaussian_exit_only(gv, O):
+    g = one_gaussian(scale=1.0, opacity=2.0, fdc=(0.5, 0.5, 0.5))
+    e = O.enclose(g)
+    vi, pi = gv.camera.pinhole((0.0, 0.0, 0.5), (0.0, 0.0, -1.0), (0.0, 1.0, 0.0), 60.0, 1.0)
+    out = O.render(e, vi, pi, 4, 4, proxy_mode=0)
+    assert (out["rgba32f"][..., 3] == 1.0).all()
+    assert (out["stats"][..., 0] == 1).all()
+
+
+def test_literal_vs_drop_rejected_and_analytic(gv, O):
+    z = np.load(os.path.join(GOLD, "config1_64.npz"))
+    tri, ana = z["rgba_tri"], z["rgba_analytic"]
+    # analytic icosahedron vs literal triangle soup: same images to quantisation
+    assert gv.psnr_rgb(gv.quantize_rgba8(tri), gv.quantize_rgba8(ana)) >= 60.0
+    s = gv.scene.config1()
+    e = O.enclose(s)
+    dr = O.render(e, z["view_inv"], z["proj_inv"], 64, 64, proxy_mode=0, drop_rejected=1)
+    np.testing.assert_array_equal(dr["rgba32f"], tri)  # exclusive tmin: rejected crossings never matter
+
+
+def test_golden_reproduced(gv, O):
+    z = np.load(os.path.join(GOLD, "config1_64.npz"))
+    s = gv.scene.config1()
+    e = O.enclose(s)
+    assert e["m"] == int(z["m"][0])
+    np.testing.assert_array_equal(e["src_index"], z["src_index"])
+    np.testing.assert_array_equal(e["density"][: z["density_head"].size], z["density_head"])
+    np.testing.assert_array_equal(e["sh"][: z["sh_head"].size], z["sh_head"])
+    np.testing.assert_array_equal(e["tris"][: z["tris_head"].size], z["tris_head"])
+    np.testing.assert_allclose(e["verts"][: z["verts_head"].size], z["verts_head"], rtol=0, atol=1e-6)
+    vi, pi = gv.scene.config1_camera(64, 64)
+    np.testing.assert_array_equal(vi, z["view_inv"])
+    np.testing.assert_array_equal(pi, z["proj_inv"])
+    for mode, key, kw in ((0, "rgba_tri", {}), (1, "rgba_analytic", {}),
+                          (0, "rgba_rt", dict(pixel_offset=0.5, alpha_init=1.0))):
+        r = O.render(e, vi, pi, 64, 64, proxy_mode=mode, **kw)
+        np.testing.assert_allclose(r["rgba32f"], z[key], rtol=0, atol=1e-6)
+    assert (z["rgba_rt"][..., 3] >= 1).all()  # RT pipeline alpha starts at 1
+
+
+def test_lightfield_golden_and_ray_dirs(gv, O):
+    z = np.load(os.path.join(GOLD, "lightfield_ring_24.npz"))
+    s = gv.scene.config1()
+    e = O.enclose(s)
+    vl, pl = gv.camera.lightfield_ring_rig(s["positions"], 4, 24, 24)
+    np.testing.assert_allclose(vl, z["view_inv"], rtol=0, atol=1e-7)
+    r = O.render(e, vl, pl, 24, 24, ncams=4, proxy_mode=0, pixel_offset=0.5, alpha_init=1.0, ray_dirs=True,
+                 ray_dirs_layout=1)
+    np.testing.assert_allclose(r["rgba32f"], z["rgba"], rtol=0, atol=1e-6)
+    # rayDirs[cam*H*W + y_launch*W + z_launch] with launch (cam, x, y) (raygenGaussianLightField.rgen:117-129)
+    dirs = r["ray_dirs"].reshape(4, 24, 24, 4)  # [cam][x][y]
+    cam, x, y = 2, 5, 17
+    V = vl.reshape(4, 16)[cam].reshape(4, 4).T
+    P = pl.reshape(4, 4).T
+    nd = np.array([(x + 0.5) / 24 * 2 - 1, (y + 0.5) / 24 * 2 - 1, 1.0, 1.0])
+    t = P @ nd
+    w = V[:3, :3] @ t[:3]
+    np.testing.assert_allclose(dirs[cam, x, y, :3], w / np.linalg.norm(w), atol=1e-6)
+
+
+def test_inclusive_tmin_needs_a_round_cap(gv, O):
+    """A rejected final crossing is re-found forever under an inclusive tmin:
+    the oracle's inclusive mode only terminates through max_rounds."""
+    g = one_gaussian(opacity=-9.0)  # density ~1e-4: every crossing rejected (alpha < 1/255)
+    e = O.enclose(g)
+    vi, pi = gv.camera.pinhole((0.0, 0.0, 3.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 10.0, 1.0)
+    inc = O.render(e, vi, pi, 2, 2, proxy_mode=0, tmin_inclusive=1, max_rounds=50)
+    exc = O.render(e, vi, pi, 2, 2, proxy_mode=0)
+    assert inc["stats"][0, 1, 1, 2] == 50  # hit the cap
+    assert exc["stats"][0, 1, 1, 2] <= 2   # exclusive: one round with the two crossings + an empty round
+
+
+def test_camera_math(gv):
+    cam = gv.camera
+    P = cam.perspective_vulkan_no_depth_reverse(math.radians(60), 2.0, 0.1, 10.0)
+    t = math.tan(math.radians(30))
+    assert P[0, 0] == pytest.approx(1 / (2 * t)) and P[1, 1] == pytest.approx(-1 / t)
+    assert P[3, 2] == -1 and P[2, 2] == pytest.approx(-10 / 9.9) and P[2, 3] == pytest.approx(-1 / 9.9)
+    vi, pi = cam.pinhole((1.0, 2.0, 3.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 45.0, 1.0)
+    V = vi.reshape(4, 4).T
+    Pi = pi.reshape(4, 4).T
+    np.testing.assert_allclose(V[:3, 3], [1, 2, 3], atol=1e-6)  # viewInverse[3] = eye
+    t = Pi @ np.array([0.0, 0.0, 1.0, 1.0])
+    w = V[:3, :3] @ t[:3]
+    np.testing.assert_allclose(w / np.linalg.norm(w), -np.array([1, 2, 3]) / np.linalg.norm([1, 2, 3]), atol=1e-6)
+    # ndc y = -1 (image row 0) looks up (+y in camera space): Vulkan y-flip of the modified glm
+    t = Pi @ np.array([0.0, -1.0, 1.0, 1.0])
+    assert t[1] > 0
