@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgvrt.so")
+LIB_PATH = os.environ.get("GVRT_LIB_PATH") or os.path.join(_HERE, "libgvrt.so")  # override: A/B builds
 
 GVRT_OK = 0
 STATUS_NAMES = {

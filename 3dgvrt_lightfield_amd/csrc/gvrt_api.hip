@@ -298,6 +298,11 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
     a.kopts = c->enc.opts;
     a.kernel_h = kernel_scale(1.0f, a.kmin, a.kopts & ~1u, a.kdeg) * SQRT3;
     a.sph_deg = p->sph_eval_degree;
+    // gres > r  <=>  gd^2 < ln(r)/S (S < 0); r <= 0 accepts everything, r >= 1 nothing
+    {
+        const double r = p->hit_min_gaussian_response;
+        a.gpre = r <= 0.0 ? INFINITY : (r >= 1.0 ? 0.0f : (float)(std::sqrt(std::log(r) / (double)KERNEL_S) * 1.001));
+    }
     a.width = width;
     a.height = height;
     a.ncams = ncams;
@@ -308,8 +313,8 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
     a.ray_dirs_layout = p->ray_dirs_layout;
     a.packed = out->packed;
     a.kfast = p->kbuffer_depth ? p->kbuffer_depth : (uint32_t)K_HITS;
-    if (a.kfast != 8 && a.kfast != 12 && a.kfast != 16 && a.kfast != 24)
-        return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "kbuffer_depth must be 0, 8, 12, 16 or 24");
+    if (a.kfast != 8 && a.kfast != 12 && a.kfast != 16)
+        return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "kbuffer_depth must be 0, 8, 12 or 16");
     uint64_t nwork = total_tiles;
     if (tiles) {
         std::vector<uint32_t> tl(ntiles);

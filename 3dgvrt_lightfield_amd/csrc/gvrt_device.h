@@ -82,6 +82,7 @@ struct RenderArgs {
     float pixel_offset;
     float alpha_init;
     float kernel_h;      // sqrt(3) * kernelScale (uniform when opts has no adaptive clamping)
+    float gpre;          // pre-reject bound on the squared line distance: sqrt(ln(min_response)/S) * 1.001
     float kmin;          // enclosing kernelMinResponse (adaptive clamping recomputes kS per particle)
     float kdeg;
     uint32_t kopts;

@@ -105,8 +105,14 @@ __device__ inline uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_r
 __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ inline float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 
-template <bool LITERAL, bool ADAPTIVE, int KB>
-__global__ __launch_bounds__(256) void k_render(const RenderArgs a, const Bvh4Node* __restrict__ nodes_,
+// Waves per SIMD the register allocator must fit: 4 (<= 128 VGPRs) measured fastest, ahead of 3 (no
+// spills) and 5 (heavy spills); see DESIGN.md §4.
+#ifndef GVRT_RENDER_MIN_WAVES
+#define GVRT_RENDER_MIN_WAVES 4
+#endif
+
+template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS>
+__global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const RenderArgs a, const Bvh4Node* __restrict__ nodes_,
                                                 const RenderRec* __restrict__ recs_, const float* __restrict__ sh_,
                                                 const float* __restrict__ view_inv_, const uint32_t* __restrict__ tiles_,
                                                 uint8_t* __restrict__ rgba8_, float* __restrict__ rgba32f_,
@@ -164,9 +170,12 @@ __global__ __launch_bounds__(256) void k_render(const RenderArgs a, const Bvh4No
         tminb = fmaxf(0.0f, fmaxf(fminf(t0x, t1x), fmaxf(fminf(t0y, t1y), fminf(t0z, t1z))));
         tmaxb = fminf(fmaxf(t0x, t1x), fminf(fmaxf(t0y, t1y), fmaxf(t0z, t1z)));
     }
+    const float term_cut = a.min_transmittance * 0.9999f;
     float last = fmaxf(0.0f, tminb - EPS_T);
     float T = 1.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f, calpha = a.alpha_init;
-    uint32_t nacc = 0, nproc = 0, rounds = 0;
+    // counters: only the STATS instantiation keeps them (registers); the accepted-hit count is
+    // recovered exactly from the alpha accumulator (RQ/RT alpha = alpha_init + #accepted, Q10)
+    uint32_t nproc = 0, rounds = 0;
     uint32_t w_nodes = 0, w_leaves = 0, l_leaves = 0;  // wave node visits, wave leaf visits, lane leaf tests
     bool active = valid && a.nrecs > 0 && (last <= tmaxb) && (T > a.min_transmittance);
 
@@ -176,8 +185,12 @@ __global__ __launch_bounds__(256) void k_render(const RenderArgs a, const Bvh4No
     int32_t* stack = s_stack[wid];
 
     while (__ballot(active)) {
-        if (active && a.max_rounds && rounds >= a.max_rounds) active = false;
-        if (active) ++rounds;
+        if constexpr (LITERAL) {
+            if (active && a.max_rounds && rounds >= a.max_rounds) active = false;
+        }
+        if constexpr (LITERAL || STATS) {
+            if (active) ++rounds;
+        }
         const float tlo = last + EPS_T;
         const float thi = tmaxb + EPS_T;
 #pragma unroll
@@ -188,12 +201,13 @@ __global__ __launch_bounds__(256) void k_render(const RenderArgs a, const Bvh4No
         }
 
         // ---------------- trace(): packet traversal of the 4-wide LBVH
+        float tcut = INF_DIST;  // termination-aware cull distance of this lane (see the leaf insert)
         int sp = 0;
         int32_t node = 0;
         while (true) {
             const Bvh4Node nd = nodes_[node];  // whole node, unconditionally: 2x s_load_dwordx16
-            ++w_nodes;
-            const float tc = fminf(thi, kt[KB - 1]);
+            if constexpr (STATS) ++w_nodes;
+            const float tc = fminf(fminf(thi, kt[KB - 1]), tcut);
             bool hit[4];
             float ent[4];
             uint64_t bal[4];
@@ -225,10 +239,10 @@ __global__ __launch_bounds__(256) void k_render(const RenderArgs a, const Bvh4No
                 const int32_t ck = k == 0 ? ch[0] : (k == 1 ? ch[1] : (k == 2 ? ch[2] : ch[3]));
                 {
                     const uint32_t gi = uni((uint32_t)(~ck));
-                    ++w_leaves;
+                    if constexpr (STATS) ++w_leaves;
                     const RenderRec rec = recs_[gi];  // whole record, before the lane branch: s_load_dwordx16
                     if ((bk >> lane) & 1ull) {
-                        ++l_leaves;
+                        if constexpr (STATS) ++l_leaves;
                         // ---- leaf: response (processHit's math) + analytic icosahedron clip
                         const float isx = rec.isx, isy = rec.isy, isz = rec.isz;
                         const f3 dxo = o - mk3(rec.px, rec.py, rec.pz);
@@ -238,14 +252,23 @@ __global__ __launch_bounds__(256) void k_render(const RenderArgs a, const Bvh4No
                         const f3 dk = mk3((rec.c0x * d.x + rec.c1x * d.y + rec.c2x * d.z) * isx,
                                           (rec.c0y * d.x + rec.c1y * d.y + rec.c2y * d.z) * isy,
                                           (rec.c0z * d.x + rec.c1z * d.y + rec.c2z * d.z) * isz);
-                        // particleResponse / alpha (gaussianfunctions.glsl:186-200)
+                        // Conservative pre-reject: gres > hitMinGaussianResponse needs the squared line
+                        // distance gd = |dk x ok|^2 / |dk|^2 below sqrt(ln(minResponse)/S) (a.gpre carries a
+                        // 1e-3 margin), so most proxies are rejected without the sqrt / exp below.
                         const float l2 = dk.x * dk.x + dk.y * dk.y + dk.z * dk.z;
-                        const f3 grd = l2 > 0.0f ? dk * (1.0f / sqrtf(l2)) : dk;
-                        const f3 gc = cross3(grd, ok);
-                        const float gd = gc.x * gc.x + gc.y * gc.y + gc.z * gc.z;
-                        const float gres = expf(KERNEL_S * gd * gd);
-                        const float galpha = fminf(0.99f, gres * rec.density);
-                        const bool acc = (gres > a.min_response) && (galpha > a.alpha_min);
+                        const f3 cu = cross3(dk, ok);
+                        const bool maybe = (cu.x * cu.x + cu.y * cu.y + cu.z * cu.z) < a.gpre * l2;
+                        bool acc = false;
+                        float galpha = 0.0f;
+                        if (maybe) {
+                            // particleResponse / alpha (gaussianfunctions.glsl:186-200)
+                            const f3 grd = l2 > 0.0f ? dk * (1.0f / sqrtf(l2)) : dk;
+                            const f3 gc = cross3(grd, ok);
+                            const float gd = gc.x * gc.x + gc.y * gc.y + gc.z * gc.z;
+                            const float gres = expf(KERNEL_S * gd * gd);
+                            galpha = fminf(0.99f, gres * rec.density);
+                            acc = (gres > a.min_response) && (galpha > a.alpha_min);
+                        }
                         if (LITERAL || acc) {
                             const float hk =
                                 ADAPTIVE ? kernel_scale(rec.density, a.kmin, a.kopts, a.kdeg) * SQRT3 : a.kernel_h;
@@ -274,9 +297,24 @@ __global__ __launch_bounds__(256) void k_render(const RenderArgs a, const Bvh4No
                                 const float al = acc ? galpha : -1.0f;
                                 const bool in0 = (a.tmin_inclusive ? tn >= tlo : tn > tlo) && tn <= thi;
                                 const bool in1 = (a.tmin_inclusive ? tf >= tlo : tf > tlo) && tf <= thi;
-                                const float ta = in0 ? tn : (in1 ? tf : INF_DIST);
-                                const float tb = (in0 && in1) ? tf : INF_DIST;
-                                if (ta < kt[KB - 1]) kb_insert2<KB>(ta, tb, gi, al, kt, kid, ka);
+                                const float ta = in0 && tn < tcut ? tn : (in1 && tf < tcut ? tf : INF_DIST);
+                                const float tb = (in0 && in1 && tf < tcut) ? tf : INF_DIST;
+                                if (ta < kt[KB - 1]) {
+                                    kb_insert2<KB>(ta, tb, gi, al, kt, kid, ka);
+                                    // Termination-aware cull distance: walking the sorted slots with the
+                                    // composite's T update, the first slot after which T <= minTransmittance
+                                    // is the last one that can ever be composited (the loop ends there), so
+                                    // nothing farther is needed.  The 1e-4 margin keeps the bound
+                                    // conservative against ulp differences from the composite's arithmetic.
+                                    float Tp = T, tt = INF_DIST;
+#pragma unroll
+                                    for (int i = 0; i < KB; ++i) {
+                                        const bool acc_i = kid[i] != INVALID_ID && ka[i] > 0.0f;
+                                        Tp = acc_i ? Tp * (1.0f - ka[i]) : Tp;
+                                        tt = (tt == INF_DIST && acc_i && Tp < term_cut) ? kt[i] : tt;
+                                    }
+                                    tcut = fminf(tcut, tt);
+                                }
                             }
                         }
                     }
@@ -337,7 +375,7 @@ __global__ __launch_bounds__(256) void k_render(const RenderArgs a, const Bvh4No
 #pragma unroll 1
                 for (int it = 0; it < KB; ++it) {
                     if (kid[0] != INVALID_ID && T > a.min_transmittance) {
-                        ++nproc;
+                        if constexpr (STATS) ++nproc;
                         if (ka[0] > 0.0f) {
                             const float weight = ka[0] * T;
                             const float4* s4 = reinterpret_cast<const float4*>(sh_ + 48ull * kid[0]);
@@ -389,7 +427,6 @@ __global__ __launch_bounds__(256) void k_render(const RenderArgs a, const Bvh4No
                             cb += rb * weight;
                             calpha += 1.0f;
                             T *= (1.0f - ka[0]);
-                            ++nacc;
                         }
                         last = fmaxf(last, kt[0]);
                     }
@@ -415,7 +452,7 @@ __global__ __launch_bounds__(256) void k_render(const RenderArgs a, const Bvh4No
             auto q8 = [](float f) -> uint32_t { return (uint32_t)(fminf(fmaxf(f, 0.0f), 1.0f) * 255.0f + 0.5f); };
             reinterpret_cast<uint32_t*>(rgba8_)[oi] = q8(cr) | (q8(cg) << 8) | (q8(cb) << 16) | (q8(calpha) << 24);
         }
-        if (hit_counts_) hit_counts_[oi] = nacc;
+        if (hit_counts_) hit_counts_[oi] = (uint32_t)(calpha - a.alpha_init);
         if (ray_dirs_) {
             const uint64_t di = a.ray_dirs_layout == 1
                                     ? ((uint64_t)cam * a.width * a.height + (uint64_t)px * a.height + py)
@@ -428,8 +465,8 @@ __global__ __launch_bounds__(256) void k_render(const RenderArgs a, const Bvh4No
         if (rgba8_) reinterpret_cast<uint32_t*>(rgba8_)[oi] = 0u;
         if (hit_counts_) hit_counts_[oi] = 0u;
     }
-    if (stats_) {
-        unsigned long long s0 = nproc, s1 = nacc, s2 = rounds, s5 = l_leaves;
+    if constexpr (STATS) {
+        unsigned long long s0 = nproc, s1 = valid ? (uint32_t)(calpha - a.alpha_init) : 0u, s2 = rounds, s5 = l_leaves;
         for (int off = 32; off > 0; off >>= 1) {
             s0 += __shfl_xor(s0, off);
             s1 += __shfl_xor(s1, off);
@@ -471,20 +508,25 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
     // every pointer is its own __restrict__ argument: the uniform node / record loads can then be
     // proven unclobbered by the output stores and are emitted as scalar (s_load) loads
 #define KARGS a.nodes, a.recs, a.sh, a.view_inv, a.tiles, a.rgba8, a.rgba32f, a.ray_dirs, a.hit_counts, a.stats
+#define GVRT_LAUNCH(L, A, K)                                                                   \
+    do {                                                                                       \
+        if (a.stats) hipLaunchKernelGGL((k_render<L, A, K, true>), g, b, 0, c->stream, a, KARGS);  \
+        else hipLaunchKernelGGL((k_render<L, A, K, false>), g, b, 0, c->stream, a, KARGS);         \
+    } while (0)
     if (literal) {  // the reference's 16-slot k-buffer (MAX_HIT_PER_TRACE)
-        if (adaptive) hipLaunchKernelGGL((k_render<true, true, K_HITS>), g, b, 0, c->stream, a, KARGS);
-        else hipLaunchKernelGGL((k_render<true, false, K_HITS>), g, b, 0, c->stream, a, KARGS);
+        if (adaptive) GVRT_LAUNCH(true, true, K_HITS);
+        else GVRT_LAUNCH(true, false, K_HITS);
     } else if (adaptive) {
-        hipLaunchKernelGGL((k_render<false, true, K_HITS>), g, b, 0, c->stream, a, KARGS);
+        GVRT_LAUNCH(false, true, K_HITS);
     } else {
         // FAST: the k-buffer depth only sets the number of traversal rounds, not the image
         switch (a.kfast) {
-            case 8: hipLaunchKernelGGL((k_render<false, false, 8>), g, b, 0, c->stream, a, KARGS); break;
-            case 12: hipLaunchKernelGGL((k_render<false, false, 12>), g, b, 0, c->stream, a, KARGS); break;
-            case 24: hipLaunchKernelGGL((k_render<false, false, 24>), g, b, 0, c->stream, a, KARGS); break;
-            default: hipLaunchKernelGGL((k_render<false, false, K_HITS>), g, b, 0, c->stream, a, KARGS); break;
+            case 8: GVRT_LAUNCH(false, false, 8); break;
+            case 12: GVRT_LAUNCH(false, false, 12); break;
+            default: GVRT_LAUNCH(false, false, K_HITS); break;
         }
     }
+#undef GVRT_LAUNCH
     GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;
 }
