@@ -6,8 +6,8 @@
 // (the render kernel clips the ray against the analytic icosahedron), so the tree has M leaves.
 //
 //   1. centroid bounds        (block reduction + ordered-uint atomics)
-//   2. 30-bit Morton codes    (10 bits per axis)
-//   3. stable radix sort      (rocPRIM via hipcub, keys 30 bits, values = compaction index)
+//   2. 63-bit Morton codes    (21 bits per axis)
+//   3. stable radix sort      (rocPRIM via hipcub, keys 63 bits, values = compaction index)
 //   4. permute records        (render records, SH, boxes into leaf order: leaf j = record j)
 //   5. Karras 2012 hierarchy  (one thread per internal node; index tie-break for equal codes)
 //   6. bottom-up AABB refit   (one thread per leaf; agent-scope acq_rel arrival counters)
@@ -62,27 +62,32 @@ __global__ __launch_bounds__(256) void k_bounds(uint64_t m, const float* __restr
     }
 }
 
-__device__ inline uint32_t expand10(uint32_t v) {
-    v = (v * 0x00010001u) & 0xFF0000FFu;
-    v = (v * 0x00000101u) & 0x0F00F00Fu;
-    v = (v * 0x00000011u) & 0xC30C30C3u;
-    v = (v * 0x00000005u) & 0x49249249u;
+// spread the low 21 bits of v to every third bit of a 64-bit word
+__device__ inline uint64_t expand21(uint64_t v) {
+    v &= 0x1FFFFFull;
+    v = (v | (v << 32)) & 0x1F00000000FFFFull;
+    v = (v | (v << 16)) & 0x1F0000FF0000FFull;
+    v = (v | (v << 8)) & 0x100F00F00F00F00Full;
+    v = (v | (v << 4)) & 0x10C30C30C30C30C3ull;
+    v = (v | (v << 2)) & 0x1249249249249249ull;
     return v;
 }
 
+// 63-bit Morton codes (21 bits per axis): at 1 M proxies a 30-bit grid leaves many equal codes in the
+// dense object region, whose order (by index) is spatially arbitrary
 __global__ __launch_bounds__(256) void k_morton(uint64_t m, const float* __restrict__ boxes, const uint32_t* __restrict__ bnd,
-                                                uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+                                                uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
-    uint32_t code = 0;
+    uint64_t code = 0;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const float lo = ord2f(bnd[k]), hi = ord2f(bnd[3 + k]);
         const float c = 0.5f * (boxes[6 * i + k] + boxes[6 * i + 3 + k]);
         const float ext = hi - lo;
         float u = ext > 0.0f ? (c - lo) / ext : 0.5f;
-        u = fminf(fmaxf(u * 1024.0f, 0.0f), 1023.0f);
-        code |= expand10((uint32_t)u) << (2 - k);
+        u = fminf(fmaxf(u * 2097152.0f, 0.0f), 2097151.0f);
+        code |= expand21((uint64_t)u) << (2 - k);
     }
     keys[i] = code;
     vals[i] = (uint32_t)i;
@@ -105,15 +110,15 @@ __global__ __launch_bounds__(256) void k_permute(uint64_t m, const uint32_t* __r
     leaf_src[j] = s;
 }
 
-__device__ inline int delta(const uint32_t* __restrict__ codes, int64_t m, int64_t i, int64_t j) {
+__device__ inline int delta(const uint64_t* __restrict__ codes, int64_t m, int64_t i, int64_t j) {
     if (j < 0 || j >= m) return -1;
-    const uint32_t a = codes[i], b = codes[j];
-    if (a == b) return 32 + __clz((uint32_t)(i ^ j));
-    return __clz(a ^ b);
+    const uint64_t a = codes[i], b = codes[j];
+    if (a == b) return 64 + __clz((uint32_t)(i ^ j));
+    return __clzll(a ^ b);
 }
 
 // Karras, "Maximizing Parallelism in the Construction of BVHs, Octrees, and k-d Trees", HPG 2012.
-__global__ __launch_bounds__(256) void k_karras(int64_t m, const uint32_t* __restrict__ codes, BvhNode* __restrict__ nodes,
+__global__ __launch_bounds__(256) void k_karras(int64_t m, const uint64_t* __restrict__ codes, BvhNode* __restrict__ nodes,
                                                 int32_t* __restrict__ leaf_parent, int32_t* __restrict__ node_parent) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m - 1) return;
@@ -289,8 +294,8 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
     if ((s = gvrt_dalloc(c, (void**)&c->d_leaf_src, 4ull * m))) return s;
 
     // scratch
-    uint32_t *bnd = nullptr, *keys = nullptr, *vals = nullptr, *keys2 = nullptr, *vals2 = nullptr, *counters = nullptr,
-             *dep = nullptr;
+    uint32_t *bnd = nullptr, *vals = nullptr, *vals2 = nullptr, *counters = nullptr, *dep = nullptr;
+    uint64_t *keys = nullptr, *keys2 = nullptr;
     int32_t *lpar = nullptr, *npar = nullptr;
     float* lboxes = nullptr;
     void* tmp = nullptr;
@@ -323,9 +328,9 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
         }                                               \
     } while (0)
     TRY(gvrt_dalloc(c, (void**)&bnd, 32));
-    TRY(gvrt_dalloc(c, (void**)&keys, 4ull * m));
+    TRY(gvrt_dalloc(c, (void**)&keys, 8ull * m));
     TRY(gvrt_dalloc(c, (void**)&vals, 4ull * m));
-    TRY(gvrt_dalloc(c, (void**)&keys2, 4ull * m));
+    TRY(gvrt_dalloc(c, (void**)&keys2, 8ull * m));
     TRY(gvrt_dalloc(c, (void**)&vals2, 4ull * m));
     TRY(gvrt_dalloc(c, (void**)&counters, 4ull * ninternal));
     TRY(gvrt_dalloc(c, (void**)&dep, 16));
@@ -342,10 +347,10 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
     hipLaunchKernelGGL(k_morton, dim3(blocks), dim3(256), 0, c->stream, (uint64_t)m, c->d_boxes_c, bnd, keys, vals);
     TRYH(hipGetLastError(), "k_morton");
     size_t tmp_bytes = 0;
-    TRYH(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys2, vals, vals2, (int)m, 0, 30, c->stream),
+    TRYH(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys2, vals, vals2, (int)m, 0, 63, c->stream),
          "SortPairs size");
     TRY(gvrt_dalloc(c, &tmp, tmp_bytes ? tmp_bytes : 16));
-    TRYH(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys2, vals, vals2, (int)m, 0, 30, c->stream),
+    TRYH(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys2, vals, vals2, (int)m, 0, 63, c->stream),
          "SortPairs");
     hipLaunchKernelGGL(k_permute, dim3(blocks), dim3(256), 0, c->stream, (uint64_t)m, vals2, c->d_recs_c, c->d_sh48,
                        c->d_boxes_c, c->d_recs, c->d_sh, lboxes, c->d_leaf_src);
@@ -379,23 +384,24 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
         TRYH(hipMemcpyAsync(&hd, dep, 4, hipMemcpyDeviceToHost, c->stream), "depth");
         // ---- collapse to the 4-wide tree (reuse keys/vals as flags / scan)
         const int64_t ni = m - 1;
+        uint32_t* flags = reinterpret_cast<uint32_t*>(keys);
         hipLaunchKernelGGL(k_even_flags, dim3((unsigned)((ni + 1 + 255) / 256)), dim3(256), 0, c->stream, ni, npar,
-                           keys);
+                           flags);
         size_t sb = 0;
-        TRYH(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, keys, vals, (int)(ni + 1), c->stream), "scan size");
+        TRYH(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, flags, vals, (int)(ni + 1), c->stream), "scan size");
         if (sb > tmp_bytes) {
             gvrt_dfree(c, &tmp);
             TRY(gvrt_dalloc(c, &tmp, sb));
             tmp_bytes = sb;
         }
-        TRYH(hipcub::DeviceScan::ExclusiveSum(tmp, sb, keys, vals, (int)(ni + 1), c->stream), "scan");
+        TRYH(hipcub::DeviceScan::ExclusiveSum(tmp, sb, flags, vals, (int)(ni + 1), c->stream), "scan");
         uint32_t n4 = 0;
         TRYH(hipMemcpyAsync(&n4, vals + ni, 4, hipMemcpyDeviceToHost, c->stream), "n4");
         TRYH(hipStreamSynchronize(c->stream), "sync");
         c->depth = hd;
         TRY(gvrt_dalloc(c, (void**)&c->d_nodes4, sizeof(Bvh4Node) * (n4 ? n4 : 1)));
         hipLaunchKernelGGL(k_collapse, dim3((unsigned)((ni + 255) / 256)), dim3(256), 0, c->stream, ni, c->d_nodes,
-                           keys, vals, c->d_nodes4);
+                           flags, vals, c->d_nodes4);
         TRYH(hipGetLastError(), "k_collapse");
         c->n_nodes4 = n4;
     }

@@ -41,15 +41,37 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
                 SH_C3_3 = 0.3731763325901154f, SH_C3_4 = -0.4570457994644658f, SH_C3_5 = 1.445305721320277f,
                 SH_C3_6 = -0.5900435899266435f;
 
-__device__ inline bool box_hit(float lx, float ly, float lz, float hx, float hy, float hz, f3 o, f3 inv, float t0,
-                               float t1, float& tenter) {
+// Build switches for A/B experiments (defaults = measured best, same-box A/B in DESIGN.md §4):
+// FMA-form slab test on (3 % faster); software prefetch of the next node / leaf record off (it made
+// every SMEM wait also cover the prefetch: SMEM returns out of order, the wait is lgkmcnt(0)).
+#ifndef GVRT_FMA_BOX
+#define GVRT_FMA_BOX 1
+#endif
+#ifndef GVRT_PREFETCH
+#define GVRT_PREFETCH 0
+#endif
+#ifndef GVRT_NODE_PREFETCH
+#define GVRT_NODE_PREFETCH 0
+#endif
+// Slab test, optionally in FMA form t = lo * inv - o * inv (one v_fma per plane).  Culling only: the proxy boxes
+// are padded (1e-5 extent + 1e-6 |centre|, gvrt_enclose.hip) and a relative slack on the exit
+// distance absorbs the rounding, so a crossing is never dropped.
+__device__ inline bool box_hit(float lx, float ly, float lz, float hx, float hy, float hz, f3 o, f3 oinv, f3 inv,
+                               float t0, float t1, float& tenter) {
+#if GVRT_FMA_BOX
+    (void)o;
+    const float ax = fmaf(lx, inv.x, -oinv.x), bx = fmaf(hx, inv.x, -oinv.x);
+    const float ay = fmaf(ly, inv.y, -oinv.y), by = fmaf(hy, inv.y, -oinv.y);
+    const float az = fmaf(lz, inv.z, -oinv.z), bz = fmaf(hz, inv.z, -oinv.z);
+#else
+    (void)oinv;
     const float ax = (lx - o.x) * inv.x, bx = (hx - o.x) * inv.x;
     const float ay = (ly - o.y) * inv.y, by = (hy - o.y) * inv.y;
     const float az = (lz - o.z) * inv.z, bz = (hz - o.z) * inv.z;
+#endif
     const float tn = fmaxf(fmaxf(t0, fminf(ax, bx)), fmaxf(fminf(ay, by), fminf(az, bz)));
     const float tf = fminf(fminf(t1, fmaxf(ax, bx)), fminf(fmaxf(ay, by), fmaxf(az, bz)));
     tenter = tn;
-    // culling only: a relative slack so rounding can never drop a crossing
     return tn <= tf + 2e-6f * fabsf(tf);
 }
 
@@ -160,6 +182,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
     const float dys = fabsf(d.y) < 1e-12f ? copysignf(1e-12f, d.y) : d.y;
     const float dzs = fabsf(d.z) < 1e-12f ? copysignf(1e-12f, d.z) : d.z;
     const f3 inv = mk3(1.0f / dxs, 1.0f / dys, 1.0f / dzs);
+    const f3 oinv = o * inv;
 
     // intersectAABB (gaussianfunctions.glsl:8-16, Q12)
     float tminb, tmaxb;
@@ -203,44 +226,99 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
         // ---------------- trace(): packet traversal of the 4-wide LBVH
         float tcut = INF_DIST;  // termination-aware cull distance of this lane (see the leaf insert)
         int sp = 0;
-        int32_t node = 0;
+        Bvh4Node nd = nodes_[0];  // whole node: 2x s_load_dwordx16
         while (true) {
-            const Bvh4Node nd = nodes_[node];  // whole node, unconditionally: 2x s_load_dwordx16
             if constexpr (STATS) ++w_nodes;
             const float tc = fminf(fminf(thi, kt[KB - 1]), tcut);
-            bool hit[4];
             float ent[4];
             uint64_t bal[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                hit[k] = box_hit(nd.lox[k], nd.loy[k], nd.loz[k], nd.hix[k], nd.hiy[k], nd.hiz[k], o, inv, tlo, tc,
-                                 ent[k]) &&
-                         active;
-                bal[k] = __ballot(hit[k]);
+                const bool hit = box_hit(nd.lox[k], nd.loy[k], nd.loz[k], nd.hix[k], nd.hiy[k], nd.hiz[k], o, oinv,
+                                         inv, tlo, tc, ent[k]) &&
+                                 active;
+                bal[k] = __ballot(hit);
             }
             int32_t ch[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) ch[k] = unii(nd.child[k]);
-            // leaves first (the k-buffer orders them); one rolled loop = one k-buffer insertion site
             uint32_t leafmask = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                if (bal[k] && ch[k] < 0) {
-                    leafmask |= 1u << k;
-                }
+                if (bal[k] && ch[k] < 0) leafmask |= 1u << k;
             }
             leafmask = uni(leafmask);
-            const uint32_t leaves_here = leafmask;
+
+            // ---- choose the next node BEFORE the leaf work, and issue its load now: the scalar
+            // load's latency then hides under this node's leaf tests (software prefetch)
+            float key[4];
+            int32_t cid[4];
+            int nint = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                key[k] = INFINITY;
+                cid[k] = -1;
+                if (bal[k] && ch[k] >= 0) {
+                    // nearest first by the entry distance of the first lane that hits the child
+                    key[k] = __shfl(ent[k], (int)__builtin_ctzll(bal[k]));
+                    cid[k] = ch[k];
+                    ++nint;
+                }
+            }
+            int32_t next = -1;
+            if (nint > 0) {
+                // sort the (key, child) pairs ascending: 5-comparator network on uniform values
+#define GVRT_CX(i, j)                                   \
+    {                                                   \
+        if (key[j] < key[i]) {                          \
+            const float tk = key[i];                    \
+            key[i] = key[j];                            \
+            key[j] = tk;                                \
+            const int32_t tc2 = cid[i];                 \
+            cid[i] = cid[j];                            \
+            cid[j] = tc2;                               \
+        }                                               \
+    }
+                GVRT_CX(0, 1) GVRT_CX(2, 3) GVRT_CX(0, 2) GVRT_CX(1, 3) GVRT_CX(1, 2)
+#undef GVRT_CX
+                for (int k = nint - 1; k >= 1; --k) {
+                    stack[sp] = cid[k];
+                    ++sp;
+                }
+                next = unii(cid[0]);
+            } else if (sp > 0) {
+                --sp;
+                next = unii(stack[sp]);
+            }
+#if GVRT_NODE_PREFETCH
+            Bvh4Node nd_next;
+            if (next >= 0) nd_next = nodes_[next];
+#endif
+
+            // ---- leaves of this node (the k-buffer orders them); one rolled loop = one insertion
+            // site; the next leaf's record load is issued before the current leaf's tests
+#if GVRT_PREFETCH
+            RenderRec rec_next;
+            if (leafmask) rec_next = recs_[~ch[__builtin_ctz(leafmask)]];
+#endif
 #pragma unroll 1
             while (leafmask) {
                 const int k = __builtin_ctz(leafmask);
                 leafmask &= leafmask - 1;
                 const uint64_t bk = k == 0 ? bal[0] : (k == 1 ? bal[1] : (k == 2 ? bal[2] : bal[3]));
                 const int32_t ck = k == 0 ? ch[0] : (k == 1 ? ch[1] : (k == 2 ? ch[2] : ch[3]));
+#if GVRT_PREFETCH
+                const RenderRec rec = rec_next;
+                if (leafmask) {
+                    const int kn = __builtin_ctz(leafmask);
+                    rec_next = recs_[~(kn == 0 ? ch[0] : (kn == 1 ? ch[1] : (kn == 2 ? ch[2] : ch[3])))];
+                }
+#else
+                const RenderRec rec = recs_[~ck];
+#endif
                 {
                     const uint32_t gi = uni((uint32_t)(~ck));
                     if constexpr (STATS) ++w_leaves;
-                    const RenderRec rec = recs_[gi];  // whole record, before the lane branch: s_load_dwordx16
                     if ((bk >> lane) & 1ull) {
                         if constexpr (STATS) ++l_leaves;
                         // ---- leaf: response (processHit's math) + analytic icosahedron clip
@@ -320,50 +398,12 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                     }
                 }
             }
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if ((leaves_here >> k) & 1u) bal[k] = 0;
-            // internal children: nearest first (entry distance of the first lane that hits each)
-            float key[4];
-            int32_t cid[4];
-            int nint = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                key[k] = INFINITY;
-                cid[k] = -1;
-                if (bal[k]) {
-                    const int first = __builtin_ctzll(bal[k]);
-                    key[k] = __shfl(ent[k], first);
-                    cid[k] = ch[k];
-                    ++nint;
-                }
-            }
-            if (nint == 0) {
-                if (sp == 0) break;
-                --sp;
-                node = unii(stack[sp]);
-                continue;
-            }
-            // sort the (key, child) pairs ascending: 5-comparator network on uniform values
-#define GVRT_CX(i, j)                                   \
-    {                                                   \
-        if (key[j] < key[i]) {                          \
-            const float tk = key[i];                    \
-            key[i] = key[j];                            \
-            key[j] = tk;                                \
-            const int32_t tc2 = cid[i];                 \
-            cid[i] = cid[j];                            \
-            cid[j] = tc2;                               \
-        }                                               \
-    }
-            GVRT_CX(0, 1) GVRT_CX(2, 3) GVRT_CX(0, 2) GVRT_CX(1, 3) GVRT_CX(1, 2)
-#undef GVRT_CX
-            // cid[0..nint-1] are the hit internal children, nearest first
-            for (int k = nint - 1; k >= 1; --k) {
-                stack[sp] = cid[k];
-                ++sp;
-            }
-            node = unii(cid[0]);
+            if (next < 0) break;
+#if GVRT_NODE_PREFETCH
+            nd = nd_next;
+#else
+            nd = nodes_[next];
+#endif
         }
 
         // ---------------- process k hits (particleRendering.comp:153-187)
