@@ -123,6 +123,76 @@ __device__ inline void kb_insert2(float ta, float tb, uint32_t id, float al, flo
     }
 }
 
+// Packed FAST k-buffer: slot payload = (record id << 8) | q, q = floor(-log2(1 - alpha) * QSCALE)
+// clamped to [0, 255] (alpha <= 0.99 so the exact code is <= 255).  q only drives the termination
+// cull: its running sum never exceeds the exact optical depth, so the cull stays conservative; the
+// composite recomputes alpha from the record as processHit does (gaussianfunctions.glsl:186-200).
+constexpr float QSCALE = 38.3837f;  // 255 / log2(100), slightly low so q(0.99) <= 255
+constexpr uint32_t PK_EMPTY = 0xFFFFFFFFu;
+
+__device__ inline uint32_t alpha_code(float alpha) {
+    const float q = -__log2f(1.0f - alpha) * QSCALE - 0.02f;  // margin covers v_log_f32 error
+    return (uint32_t)fminf(fmaxf(q, 0.0f), 255.0f);
+}
+
+// As kb_insert2, with one 32-bit payload per slot (t, then payload; same strict-< rule)
+template <int K>
+__device__ inline void kb_insert2p(float ta, float tb, uint32_t pk, float (&kt)[K], uint32_t (&kp)[K]) {
+    float pt0 = ta, pt1 = tb;
+    uint32_t pp0 = pk, pp1 = pk;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const bool c0 = pt0 < kt[i];
+        const float st = kt[i];
+        const uint32_t sp = kp[i];
+        kt[i] = c0 ? pt0 : st;
+        kp[i] = c0 ? pp0 : sp;
+        const float xt = c0 ? st : pt0;
+        const uint32_t xp = c0 ? sp : pp0;
+        const bool c1 = pt1 < xt;
+        pt0 = c1 ? pt1 : xt;
+        pp0 = c1 ? pp1 : xp;
+        pt1 = c1 ? xt : pt1;
+        pp1 = c1 ? xp : pp1;
+    }
+}
+
+// Kernel-frame ray of one particle (gaussianfunctions.glsl:186-191): ok = S^-1 R^T (o - p), dk = S^-1 R^T d.
+// Written with explicit fmaf and contraction off: the insert-time and composite-time evaluations of
+// kernel_frame / particle_alpha must round identically, and the backend otherwise fuses mul+add pairs
+// differently at each inlined site (SLP-packed v_pk_fma_f32 at one, scalar mul/sub at the other).
+__device__ inline void kernel_frame(const RenderRec& rec, f3 o, f3 d, f3& ok, f3& dk) {
+#pragma clang fp contract(off)
+    const float ex = o.x - rec.px, ey = o.y - rec.py, ez = o.z - rec.pz;
+    ok = mk3(fmaf(rec.c2x, ez, fmaf(rec.c1x, ey, rec.c0x * ex)) * rec.isx,
+             fmaf(rec.c2y, ez, fmaf(rec.c1y, ey, rec.c0y * ex)) * rec.isy,
+             fmaf(rec.c2z, ez, fmaf(rec.c1z, ey, rec.c0z * ex)) * rec.isz);
+    dk = mk3(fmaf(rec.c2x, d.z, fmaf(rec.c1x, d.y, rec.c0x * d.x)) * rec.isx,
+             fmaf(rec.c2y, d.z, fmaf(rec.c1y, d.y, rec.c0y * d.x)) * rec.isy,
+             fmaf(rec.c2z, d.z, fmaf(rec.c1z, d.y, rec.c0z * d.x)) * rec.isz);
+}
+
+__device__ inline float len2(f3 v) {
+#pragma clang fp contract(off)
+    return fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x));
+}
+
+// particleResponse + alpha + the accept test (gaussianfunctions.glsl:192-200); one definition so the
+// insert-time and composite-time evaluations are the same arithmetic
+__device__ inline bool particle_alpha(f3 ok, f3 dk, float l2, float density, float min_response, float alpha_min,
+                                      float& galpha) {
+#pragma clang fp contract(off)
+    const float rl = l2 > 0.0f ? 1.0f / sqrtf(l2) : 1.0f;
+    const float gx = dk.x * rl, gy = dk.y * rl, gz = dk.z * rl;
+    const float cx = fmaf(gy, ok.z, -(gz * ok.y));
+    const float cy = fmaf(gz, ok.x, -(gx * ok.z));
+    const float cz = fmaf(gx, ok.y, -(gy * ok.x));
+    const float gd = fmaf(cz, cz, fmaf(cy, cy, cx * cx));
+    const float gres = expf((KERNEL_S * gd) * gd);
+    galpha = fminf(0.99f, gres * density);
+    return (gres > min_response) && (galpha > alpha_min);
+}
+
 __device__ inline uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ inline float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
@@ -133,7 +203,7 @@ __device__ inline float unif(float v) { return __int_as_float(__builtin_amdgcn_r
 #define GVRT_RENDER_MIN_WAVES 4
 #endif
 
-template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS>
+template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK>
 __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const RenderArgs a, const Bvh4Node* __restrict__ nodes_,
                                                 const RenderRec* __restrict__ recs_, const float* __restrict__ sh_,
                                                 const float* __restrict__ view_inv_, const uint32_t* __restrict__ tiles_,
@@ -202,9 +272,10 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
     uint32_t w_nodes = 0, w_leaves = 0, l_leaves = 0;  // wave node visits, wave leaf visits, lane leaf tests
     bool active = valid && a.nrecs > 0 && (last <= tmaxb) && (T > a.min_transmittance);
 
+    static_assert(!(LITERAL && PACK), "LITERAL keeps rejected crossings: unpacked k-buffer");
     float kt[KB];
-    uint32_t kid[KB];
-    float ka[KB];
+    uint32_t kid[KB];       // record id, or the packed payload (id << 8 | q) when PACK
+    float ka[PACK ? 1 : KB];  // alpha per slot (unpacked only; < 0 = rejected crossing in LITERAL)
     int32_t* stack = s_stack[wid];
 
     while (__ballot(active)) {
@@ -219,8 +290,15 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
 #pragma unroll
         for (int i = 0; i < KB; ++i) {
             kt[i] = INF_DIST;
-            kid[i] = INVALID_ID;
-            ka[i] = 0.0f;  // never read for an empty slot, but keeps the register set defined
+            kid[i] = PACK ? PK_EMPTY : INVALID_ID;  // same all-ones value
+            if constexpr (!PACK) ka[i] = 0.0f;  // never read for an empty slot, but keeps the register set defined
+        }
+        // PACK: optical-depth budget of this round in q units; a slot whose running q sum reaches it
+        // drives T below minTransmittance (q sums never exceed the exact depth; +0.5 q of margin)
+        uint32_t qneed = 0;
+        if constexpr (PACK) {
+            const float need = T > term_cut ? __log2f(T / term_cut) * QSCALE + 0.5f : 0.0f;
+            qneed = (uint32_t)fminf(ceilf(need), 4.0e9f);
         }
 
         // ---------------- trace(): packet traversal of the 4-wide LBVH
@@ -322,31 +400,17 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                     if ((bk >> lane) & 1ull) {
                         if constexpr (STATS) ++l_leaves;
                         // ---- leaf: response (processHit's math) + analytic icosahedron clip
-                        const float isx = rec.isx, isy = rec.isy, isz = rec.isz;
-                        const f3 dxo = o - mk3(rec.px, rec.py, rec.pz);
-                        const f3 ok = mk3((rec.c0x * dxo.x + rec.c1x * dxo.y + rec.c2x * dxo.z) * isx,
-                                          (rec.c0y * dxo.x + rec.c1y * dxo.y + rec.c2y * dxo.z) * isy,
-                                          (rec.c0z * dxo.x + rec.c1z * dxo.y + rec.c2z * dxo.z) * isz);
-                        const f3 dk = mk3((rec.c0x * d.x + rec.c1x * d.y + rec.c2x * d.z) * isx,
-                                          (rec.c0y * d.x + rec.c1y * d.y + rec.c2y * d.z) * isy,
-                                          (rec.c0z * d.x + rec.c1z * d.y + rec.c2z * d.z) * isz);
+                        f3 ok, dk;
+                        kernel_frame(rec, o, d, ok, dk);
                         // Conservative pre-reject: gres > hitMinGaussianResponse needs the squared line
                         // distance gd = |dk x ok|^2 / |dk|^2 below sqrt(ln(minResponse)/S) (a.gpre carries a
                         // 1e-3 margin), so most proxies are rejected without the sqrt / exp below.
-                        const float l2 = dk.x * dk.x + dk.y * dk.y + dk.z * dk.z;
+                        const float l2 = len2(dk);
                         const f3 cu = cross3(dk, ok);
                         const bool maybe = (cu.x * cu.x + cu.y * cu.y + cu.z * cu.z) < a.gpre * l2;
                         bool acc = false;
                         float galpha = 0.0f;
-                        if (maybe) {
-                            // particleResponse / alpha (gaussianfunctions.glsl:186-200)
-                            const f3 grd = l2 > 0.0f ? dk * (1.0f / sqrtf(l2)) : dk;
-                            const f3 gc = cross3(grd, ok);
-                            const float gd = gc.x * gc.x + gc.y * gc.y + gc.z * gc.z;
-                            const float gres = expf(KERNEL_S * gd * gd);
-                            galpha = fminf(0.99f, gres * rec.density);
-                            acc = (gres > a.min_response) && (galpha > a.alpha_min);
-                        }
+                        if (maybe) acc = particle_alpha(ok, dk, l2, rec.density, a.min_response, a.alpha_min, galpha);
                         if (LITERAL || acc) {
                             const float hk =
                                 ADAPTIVE ? kernel_scale(rec.density, a.kmin, a.kopts, a.kdeg) * SQRT3 : a.kernel_h;
@@ -378,6 +442,19 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                                 const float ta = in0 && tn < tcut ? tn : (in1 && tf < tcut ? tf : INF_DIST);
                                 const float tb = (in0 && in1 && tf < tcut) ? tf : INF_DIST;
                                 if (ta < kt[KB - 1]) {
+                                  if constexpr (PACK) {
+                                    kb_insert2p<KB>(ta, tb, (gi << 8) | alpha_code(galpha), kt, kid);
+                                    // termination cull on the q codes (see kb_insert2p): the first slot
+                                    // whose running sum reaches qneed is the last one composited
+                                    uint32_t qs = 0;
+                                    float tt = INF_DIST;
+#pragma unroll
+                                    for (int i = 0; i < KB; ++i) {
+                                        qs += kid[i] & 0xFFu;
+                                        tt = fminf(tt, qs >= qneed ? kt[i] : INF_DIST);
+                                    }
+                                    tcut = fminf(tcut, tt);
+                                  } else {
                                     kb_insert2<KB>(ta, tb, gi, al, kt, kid, ka);
                                     // Termination-aware cull distance: walking the sorted slots with the
                                     // composite's T update, the first slot after which T <= minTransmittance
@@ -392,6 +469,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                                         tt = (tt == INF_DIST && acc_i && Tp < term_cut) ? kt[i] : tt;
                                     }
                                     tcut = fminf(tcut, tt);
+                                  }
                                 }
                             }
                         }
@@ -416,9 +494,25 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                 for (int it = 0; it < KB; ++it) {
                     if (kid[0] != INVALID_ID && T > a.min_transmittance) {
                         if constexpr (STATS) ++nproc;
-                        if (ka[0] > 0.0f) {
-                            const float weight = ka[0] * T;
-                            const float4* s4 = reinterpret_cast<const float4*>(sh_ + 48ull * kid[0]);
+                        uint32_t hid;
+                        float halpha;
+                        bool hacc;
+                        if constexpr (PACK) {
+                            // processHit re-evaluates the response of the hit particle (per-lane record load)
+                            hid = kid[0] >> 8;
+                            const RenderRec rec = recs_[hid];
+                            f3 ok, dk;
+                            kernel_frame(rec, o, d, ok, dk);
+                            const float l2 = len2(dk);
+                            hacc = particle_alpha(ok, dk, l2, rec.density, a.min_response, a.alpha_min, halpha);
+                        } else {
+                            hid = kid[0];
+                            halpha = ka[0];
+                            hacc = ka[0] > 0.0f;
+                        }
+                        if (hacc) {
+                            const float weight = halpha * T;
+                            const float4* s4 = reinterpret_cast<const float4*>(sh_ + 48ull * hid);
                             float rr = 0.f, rg = 0.f, rb = 0.f;
                             // 16 coefficients x rgb = 12 float4, in 4 rolled chunks of 3 (few live VGPRs)
 #pragma unroll 1
@@ -466,7 +560,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                             cg += rg * weight;
                             cb += rb * weight;
                             calpha += 1.0f;
-                            T *= (1.0f - ka[0]);
+                            T *= (1.0f - halpha);
                         }
                         last = fmaxf(last, kt[0]);
                     }
@@ -474,7 +568,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                     for (int i = 0; i < KB - 1; ++i) {
                         kt[i] = kt[i + 1];
                         kid[i] = kid[i + 1];
-                        ka[i] = ka[i + 1];
+                        if constexpr (!PACK) ka[i] = ka[i + 1];
                     }
                     kid[KB - 1] = INVALID_ID;
                 }
@@ -548,22 +642,27 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
     // every pointer is its own __restrict__ argument: the uniform node / record loads can then be
     // proven unclobbered by the output stores and are emitted as scalar (s_load) loads
 #define KARGS a.nodes, a.recs, a.sh, a.view_inv, a.tiles, a.rgba8, a.rgba32f, a.ray_dirs, a.hit_counts, a.stats
-#define GVRT_LAUNCH(L, A, K)                                                                   \
-    do {                                                                                       \
-        if (a.stats) hipLaunchKernelGGL((k_render<L, A, K, true>), g, b, 0, c->stream, a, KARGS);  \
-        else hipLaunchKernelGGL((k_render<L, A, K, false>), g, b, 0, c->stream, a, KARGS);         \
+#define GVRT_LAUNCH(L, A, K, P)                                                                    \
+    do {                                                                                           \
+        if (a.stats) hipLaunchKernelGGL((k_render<L, A, K, true, P>), g, b, 0, c->stream, a, KARGS);  \
+        else hipLaunchKernelGGL((k_render<L, A, K, false, P>), g, b, 0, c->stream, a, KARGS);         \
     } while (0)
+    // packed payload needs record ids below 2^24 - 1 (id << 8 | q, all-ones = empty slot)
+    const bool pack = a.nrecs < 0xFFFFFFu;
     if (literal) {  // the reference's 16-slot k-buffer (MAX_HIT_PER_TRACE)
-        if (adaptive) GVRT_LAUNCH(true, true, K_HITS);
-        else GVRT_LAUNCH(true, false, K_HITS);
+        if (adaptive) GVRT_LAUNCH(true, true, K_HITS, false);
+        else GVRT_LAUNCH(true, false, K_HITS, false);
+    } else if (!pack) {
+        if (adaptive) GVRT_LAUNCH(false, true, K_HITS, false);
+        else GVRT_LAUNCH(false, false, K_HITS, false);
     } else if (adaptive) {
-        GVRT_LAUNCH(false, true, K_HITS);
+        GVRT_LAUNCH(false, true, K_HITS, true);
     } else {
         // FAST: the k-buffer depth only sets the number of traversal rounds, not the image
         switch (a.kfast) {
-            case 8: GVRT_LAUNCH(false, false, 8); break;
-            case 12: GVRT_LAUNCH(false, false, 12); break;
-            default: GVRT_LAUNCH(false, false, K_HITS); break;
+            case 8: GVRT_LAUNCH(false, false, 8, true); break;
+            case 12: GVRT_LAUNCH(false, false, 12, true); break;
+            default: GVRT_LAUNCH(false, false, K_HITS, true); break;
         }
     }
 #undef GVRT_LAUNCH
