@@ -50,6 +50,9 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 #ifndef GVRT_PREFETCH
 #define GVRT_PREFETCH 0
 #endif
+#ifndef GVRT_APPROX_RESPONSE
+#define GVRT_APPROX_RESPONSE 0
+#endif
 #ifndef GVRT_NODE_PREFETCH
 #define GVRT_NODE_PREFETCH 0
 #endif
@@ -182,13 +185,21 @@ __device__ inline float len2(f3 v) {
 __device__ inline bool particle_alpha(f3 ok, f3 dk, float l2, float density, float min_response, float alpha_min,
                                       float& galpha) {
 #pragma clang fp contract(off)
+#if GVRT_APPROX_RESPONSE
+    const float rl = l2 > 0.0f ? __builtin_amdgcn_rsqf(l2) : 1.0f;
+#else
     const float rl = l2 > 0.0f ? 1.0f / sqrtf(l2) : 1.0f;
+#endif
     const float gx = dk.x * rl, gy = dk.y * rl, gz = dk.z * rl;
     const float cx = fmaf(gy, ok.z, -(gz * ok.y));
     const float cy = fmaf(gz, ok.x, -(gx * ok.z));
     const float cz = fmaf(gx, ok.y, -(gy * ok.x));
     const float gd = fmaf(cz, cz, fmaf(cy, cy, cx * cx));
+#if GVRT_APPROX_RESPONSE
+    const float gres = __expf((KERNEL_S * gd) * gd);
+#else
     const float gres = expf((KERNEL_S * gd) * gd);
+#endif
     galpha = fminf(0.99f, gres * density);
     return (gres > min_response) && (galpha > alpha_min);
 }
@@ -211,6 +222,9 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                                                 float* __restrict__ ray_dirs_, uint32_t* __restrict__ hit_counts_,
                                                 unsigned long long* __restrict__ stats_) {
     __shared__ int32_t s_stack[4][STACK_DEPTH];
+    // SH basis of each lane's ray direction, chunk-major so one ds_read_b128 per chunk is
+    // conflict-free (16 KB per block; occupancy is VGPR-bound, not LDS-bound)
+    __shared__ float4 s_basis[4][4][64];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const uint64_t tile_idx = (uint64_t)blockIdx.x * 4 + wid;
@@ -277,6 +291,26 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
     uint32_t kid[KB];       // record id, or the packed payload (id << 8 | q) when PACK
     float ka[PACK ? 1 : KB];  // alpha per slot (unpacked only; < 0 = rejected crossing in LITERAL)
     int32_t* stack = s_stack[wid];
+    {
+        // radianceFromSpH basis factors (gaussianfunctions.glsl:122-151), signs folded, zero past
+        // sph_eval_degree; computed once per ray and kept in LDS (not registers) through the traversal
+        const float x = d.x, y = d.y, z = d.z;
+        const uint32_t deg = a.sph_deg;
+        const float xx = x * x, yy = y * y, zz = z * z;
+        s_basis[wid][0][lane] = make_float4(SH_C0, deg > 0 ? -(SH_C1 * y) : 0.f, deg > 0 ? SH_C1 * z : 0.f,
+                                            deg > 0 ? -(SH_C1 * x) : 0.f);
+        s_basis[wid][1][lane] = make_float4(deg > 1 ? SH_C2_0 * (x * y) : 0.f, deg > 1 ? SH_C2_1 * (y * z) : 0.f,
+                                            deg > 1 ? SH_C2_2 * (2.0f * zz - xx - yy) : 0.f,
+                                            deg > 1 ? SH_C2_3 * (x * z) : 0.f);
+        s_basis[wid][2][lane] = make_float4(deg > 1 ? SH_C2_4 * (xx - yy) : 0.f,
+                                            deg > 2 ? SH_C3_0 * y * (3.0f * xx - yy) : 0.f,
+                                            deg > 2 ? SH_C3_1 * (x * y) * z : 0.f,
+                                            deg > 2 ? SH_C3_2 * y * (4.0f * zz - xx - yy) : 0.f);
+        s_basis[wid][3][lane] = make_float4(deg > 2 ? SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) : 0.f,
+                                            deg > 2 ? SH_C3_4 * x * (4.0f * zz - xx - yy) : 0.f,
+                                            deg > 2 ? SH_C3_5 * z * (xx - yy) : 0.f,
+                                            deg > 2 ? SH_C3_6 * x * (xx - 3.0f * yy) : 0.f);
+    }
 
     while (__ballot(active)) {
         if constexpr (LITERAL) {
@@ -492,7 +526,9 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                 // rolled loop over slots: composite slot 0, then shift the buffer down by one
 #pragma unroll 1
                 for (int it = 0; it < KB; ++it) {
-                    if (kid[0] != INVALID_ID && T > a.min_transmittance) {
+                    // slots are sorted with the empty ones last, and T only falls: this lane is done
+                    if (!(kid[0] != INVALID_ID && T > a.min_transmittance)) break;
+                    {
                         if constexpr (STATS) ++nproc;
                         uint32_t hid;
                         float halpha;
@@ -518,35 +554,8 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
 #pragma unroll 1
                             for (int q = 0; q < 4; ++q) {
                                 const float4 v0 = s4[3 * q], v1 = s4[3 * q + 1], v2 = s4[3 * q + 2];
-                                // basis factors 4q..4q+3 of radianceFromSpH (gaussianfunctions.glsl:122-151),
-                                // signs folded, zero past sph_eval_degree; recomputed per chunk so they
-                                // are not held in registers through the traversal
-                                float x = d.x, y = d.y, z = d.z;
-                                asm volatile("" : "+v"(x), "+v"(y), "+v"(z));  // keep LICM from hoisting 16 factors
-                                const uint32_t deg = a.sph_deg;
-                                const float xx = x * x, yy = y * y, zz = z * z;
-                                float b0, b1, b2, b3;
-                                if (q == 0) {
-                                    b0 = SH_C0;
-                                    b1 = deg > 0 ? -(SH_C1 * y) : 0.f;
-                                    b2 = deg > 0 ? SH_C1 * z : 0.f;
-                                    b3 = deg > 0 ? -(SH_C1 * x) : 0.f;
-                                } else if (q == 1) {
-                                    b0 = deg > 1 ? SH_C2_0 * (x * y) : 0.f;
-                                    b1 = deg > 1 ? SH_C2_1 * (y * z) : 0.f;
-                                    b2 = deg > 1 ? SH_C2_2 * (2.0f * zz - xx - yy) : 0.f;
-                                    b3 = deg > 1 ? SH_C2_3 * (x * z) : 0.f;
-                                } else if (q == 2) {
-                                    b0 = deg > 1 ? SH_C2_4 * (xx - yy) : 0.f;
-                                    b1 = deg > 2 ? SH_C3_0 * y * (3.0f * xx - yy) : 0.f;
-                                    b2 = deg > 2 ? SH_C3_1 * (x * y) * z : 0.f;
-                                    b3 = deg > 2 ? SH_C3_2 * y * (4.0f * zz - xx - yy) : 0.f;
-                                } else {
-                                    b0 = deg > 2 ? SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) : 0.f;
-                                    b1 = deg > 2 ? SH_C3_4 * x * (4.0f * zz - xx - yy) : 0.f;
-                                    b2 = deg > 2 ? SH_C3_5 * z * (xx - yy) : 0.f;
-                                    b3 = deg > 2 ? SH_C3_6 * x * (xx - 3.0f * yy) : 0.f;
-                                }
+                                const float4 bq = s_basis[wid][q][lane];
+                                const float b0 = bq.x, b1 = bq.y, b2 = bq.z, b3 = bq.w;
                                 // coefficients 4q..4q+3: (v0.xyz) (v0.w v1.xy) (v1.zw v2.x) (v2.yzw)
                                 rr += b0 * v0.x; rg += b0 * v0.y; rb += b0 * v0.z;
                                 rr += b1 * v0.w; rg += b1 * v1.x; rb += b1 * v1.y;
