@@ -51,7 +51,7 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 #define GVRT_PREFETCH 0
 #endif
 #ifndef GVRT_APPROX_RESPONSE
-#define GVRT_APPROX_RESPONSE 0
+#define GVRT_APPROX_RESPONSE 1
 #endif
 #ifndef GVRT_NODE_PREFETCH
 #define GVRT_NODE_PREFETCH 0
@@ -337,6 +337,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
 
         // ---------------- trace(): packet traversal of the 4-wide LBVH
         float tcut = INF_DIST;  // termination-aware cull distance of this lane (see the leaf insert)
+        const uint64_t amask = __builtin_amdgcn_ballot_w64(active);
         int sp = 0;
         Bvh4Node nd = nodes_[0];  // whole node: 2x s_load_dwordx16
         while (true) {
@@ -347,9 +348,8 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const bool hit = box_hit(nd.lox[k], nd.loy[k], nd.loz[k], nd.hix[k], nd.hiy[k], nd.hiz[k], o, oinv,
-                                         inv, tlo, tc, ent[k]) &&
-                                 active;
-                bal[k] = __ballot(hit);
+                                         inv, tlo, tc, ent[k]);
+                bal[k] = __builtin_amdgcn_ballot_w64(hit) & amask;  // compare result straight to an SGPR mask
             }
             int32_t ch[4];
 #pragma unroll
@@ -361,18 +361,17 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
             }
             leafmask = uni(leafmask);
 
-            // ---- choose the next node BEFORE the leaf work, and issue its load now: the scalar
-            // load's latency then hides under this node's leaf tests (software prefetch)
-            float key[4];
+            // ---- choose the next node before the leaf work (all on uniform values: SALU)
+            uint32_t key[4];  // entry distance bits: distances are >= tlo > 0, so uint order = float order
             int32_t cid[4];
             int nint = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                key[k] = INFINITY;
+                key[k] = 0xFFFFFFFFu;
                 cid[k] = -1;
                 if (bal[k] && ch[k] >= 0) {
                     // nearest first by the entry distance of the first lane that hits the child
-                    key[k] = __shfl(ent[k], (int)__builtin_ctzll(bal[k]));
+                    key[k] = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(ent[k]), (int)__builtin_ctzll(bal[k]));
                     cid[k] = ch[k];
                     ++nint;
                 }
@@ -380,16 +379,15 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
             int32_t next = -1;
             if (nint > 0) {
                 // sort the (key, child) pairs ascending: 5-comparator network on uniform values
-#define GVRT_CX(i, j)                                   \
-    {                                                   \
-        if (key[j] < key[i]) {                          \
-            const float tk = key[i];                    \
-            key[i] = key[j];                            \
-            key[j] = tk;                                \
-            const int32_t tc2 = cid[i];                 \
-            cid[i] = cid[j];                            \
-            cid[j] = tc2;                               \
-        }                                               \
+#define GVRT_CX(i, j)                                          \
+    {                                                          \
+        const bool sw = key[j] < key[i];                       \
+        const uint32_t ki = key[i], kj = key[j];               \
+        const int32_t ci = cid[i], cj = cid[j];                \
+        key[i] = sw ? kj : ki;                                 \
+        key[j] = sw ? ki : kj;                                 \
+        cid[i] = sw ? cj : ci;                                 \
+        cid[j] = sw ? ci : cj;                                 \
     }
                 GVRT_CX(0, 1) GVRT_CX(2, 3) GVRT_CX(0, 2) GVRT_CX(1, 3) GVRT_CX(1, 2)
 #undef GVRT_CX
