@@ -204,6 +204,34 @@ __device__ inline bool particle_alpha(f3 ok, f3 dk, float l2, float density, flo
     return (gres > min_response) && (galpha > alpha_min);
 }
 
+// Entry / exit distance of a ray through the icosahedron proxy (kernel frame, inradius hk / sqrt(3) *
+// sqrt(3) = kS): the 20 faces lie on 10 antipodal slab pairs |n . x| <= hk with the normals below
+// (particlePrimitives.comp:76-79 vertices; their face planes).  Per slab the crossing interval is
+// centre m = -(n . ok) / (n . dk) +- hk / |n . dk|; the reciprocal is clamped to +-1e30 so a ray
+// parallel to a slab gives an unbounded interval when inside it and an empty one when outside.
+__device__ inline void ico_clip(f3 ok, f3 dk, float hk, float& tn, float& tf) {
+    // n . ok and n . dk for the 10 normals, sharing partial sums
+    const float pxy = ok.x + ok.y, mxy = ok.x - ok.y, qxy = dk.x + dk.y, nxy = dk.x - dk.y;
+    const float px = PHI * ok.x, py = PHI * ok.y, pz = PHI * ok.z;
+    const float qx = PHI * dk.x, qy = PHI * dk.y, qz = PHI * dk.z;
+    const float sa[10] = {pxy + ok.z, pxy - ok.z, mxy + ok.z, ok.z - mxy,
+                          fmaf(IPHI, ok.z, py), fmaf(-IPHI, ok.z, py), fmaf(IPHI, ok.x, pz), fmaf(-IPHI, ok.x, pz),
+                          fmaf(IPHI, ok.y, px), fmaf(-IPHI, ok.y, px)};
+    const float sb[10] = {qxy + dk.z, qxy - dk.z, nxy + dk.z, dk.z - nxy,
+                          fmaf(IPHI, dk.z, qy), fmaf(-IPHI, dk.z, qy), fmaf(IPHI, dk.x, qz), fmaf(-IPHI, dk.x, qz),
+                          fmaf(IPHI, dk.y, qx), fmaf(-IPHI, dk.y, qx)};
+    float lo = -INFINITY, hi = INFINITY;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const float ib = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(sb[i]), -1e30f, 1e30f);
+        const float h = hk * fabsf(ib);
+        lo = fmaxf(lo, fmaf(-sa[i], ib, -h));
+        hi = fminf(hi, fmaf(-sa[i], ib, h));
+    }
+    tn = lo;
+    tf = hi;
+}
+
 __device__ inline uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ inline float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
@@ -446,27 +474,8 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                         if (LITERAL || acc) {
                             const float hk =
                                 ADAPTIVE ? kernel_scale(rec.density, a.kmin, a.kopts, a.kdeg) * SQRT3 : a.kernel_h;
-                            float tn = -INFINITY, tf = INFINITY;
-#define GVRT_SLAB(AX, AY, AZ)                                      \
-    {                                                              \
-        const float sa = (AX) * ok.x + (AY) * ok.y + (AZ) * ok.z;  \
-        const float sb = (AX) * dk.x + (AY) * dk.y + (AZ) * dk.z;  \
-        const float ib = __builtin_amdgcn_rcpf(sb);                \
-        const float t1 = (-hk - sa) * ib, t2 = (hk - sa) * ib;     \
-        tn = fmaxf(tn, fminf(t1, t2));                             \
-        tf = fminf(tf, fmaxf(t1, t2));                             \
-    }
-                            GVRT_SLAB(1.f, 1.f, 1.f)
-                            GVRT_SLAB(1.f, 1.f, -1.f)
-                            GVRT_SLAB(1.f, -1.f, 1.f)
-                            GVRT_SLAB(-1.f, 1.f, 1.f)
-                            GVRT_SLAB(0.f, PHI, IPHI)
-                            GVRT_SLAB(0.f, PHI, -IPHI)
-                            GVRT_SLAB(IPHI, 0.f, PHI)
-                            GVRT_SLAB(-IPHI, 0.f, PHI)
-                            GVRT_SLAB(PHI, IPHI, 0.f)
-                            GVRT_SLAB(PHI, -IPHI, 0.f)
-#undef GVRT_SLAB
+                            float tn, tf;
+                            ico_clip(ok, dk, hk, tn, tf);
                             if (tn <= tf) {
                                 const float al = acc ? galpha : -1.0f;
                                 const bool in0 = (a.tmin_inclusive ? tn >= tlo : tn > tlo) && tn <= thi;
