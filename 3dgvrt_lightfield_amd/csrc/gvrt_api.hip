@@ -312,9 +312,9 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
     a.max_rounds = p->max_rounds;
     a.ray_dirs_layout = p->ray_dirs_layout;
     a.packed = out->packed;
-    a.kfast = p->kbuffer_depth ? p->kbuffer_depth : (uint32_t)K_HITS;
-    if (a.kfast != 8 && a.kfast != 12 && a.kfast != 16)
-        return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "kbuffer_depth must be 0, 8, 12 or 16");
+    a.kfast = p->kbuffer_depth ? p->kbuffer_depth : (uint32_t)K_FAST_DEFAULT;
+    if (a.kfast != 8 && a.kfast != 12 && a.kfast != 16 && a.kfast != 20 && a.kfast != 24 && a.kfast != 32)
+        return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "kbuffer_depth must be 0, 8, 12, 16, 20, 24 or 32");
     uint64_t nwork = total_tiles;
     if (tiles) {
         std::vector<uint32_t> tl(ntiles);

@@ -10,8 +10,8 @@
 // the LBVH: node and leaf records are addressed by a wave-uniform index and fetched with scalar
 // loads (two s_load_dwordx16 per 128-B node, one per 64-B record), every lane clips its own ray
 // against the four child boxes, and ballots decide which children the packet descends into; the
-// farther children go on a per-wave LDS stack, nearest first by the first hitting lane's entry
-// distance.  Leaves are clipped against the analytic icosahedron (10 antipodal slab pairs in the
+// farther children go on a per-wave stack held in two VGPRs (one entry per lane), nearest first by
+// the first hitting lane's entry distance.  Leaves are clipped against the analytic icosahedron (10 antipodal slab pairs in the
 // kernel frame), which yields the same two crossings (entry and exit face, Q1) as the
 // reference's 20-triangle proxy.  Each lane keeps a 16-slot register k-buffer
 // (compareAndSwapHitPayloadValue chain, anyhit.rahit:29-71); a full buffer shrinks that lane's
@@ -42,19 +42,17 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
                 SH_C3_6 = -0.5900435899266435f;
 
 // Build switches for A/B experiments (defaults = measured best, same-box A/B in DESIGN.md §4):
-// FMA-form slab test on (3 % faster); software prefetch of the next node / leaf record off (it made
-// every SMEM wait also cover the prefetch: SMEM returns out of order, the wait is lgkmcnt(0)).
+// FMA-form slab test (3 % faster); v_rsq / v_exp in the response (4 % faster, parity unchanged).
+// A software prefetch of the next node / leaf record was measured slower and removed: SMEM returns
+// out of order, so every wait on a record also waited on the prefetch (lgkmcnt(0)).
 #ifndef GVRT_FMA_BOX
 #define GVRT_FMA_BOX 1
 #endif
-#ifndef GVRT_PREFETCH
-#define GVRT_PREFETCH 0
+#ifndef GVRT_VSTACK
+#define GVRT_VSTACK 0
 #endif
 #ifndef GVRT_APPROX_RESPONSE
 #define GVRT_APPROX_RESPONSE 1
-#endif
-#ifndef GVRT_NODE_PREFETCH
-#define GVRT_NODE_PREFETCH 0
 #endif
 // Slab test, optionally in FMA form t = lo * inv - o * inv (one v_fma per plane).  Culling only: the proxy boxes
 // are padded (1e-5 extent + 1e-6 |centre|, gvrt_enclose.hip) and a relative slack on the exit
@@ -138,25 +136,34 @@ __device__ inline uint32_t alpha_code(float alpha) {
     return (uint32_t)fminf(fmaxf(q, 0.0f), 255.0f);
 }
 
-// As kb_insert2, with one 32-bit payload per slot (t, then payload; same strict-< rule)
+// As kb_insert2, with one 32-bit payload per slot (t, then payload; same strict-< rule).  The chain
+// runs in groups of 4 slots, and a group is skipped when no inserting lane has its pending crossing
+// below the group's last slot: the pending pair stays sorted (pt0 <= pt1), so such a group would not
+// change.  With front-to-back traversal most crossings land near the end of the buffer.
 template <int K>
 __device__ inline void kb_insert2p(float ta, float tb, uint32_t pk, float (&kt)[K], uint32_t (&kp)[K]) {
+    static_assert(K % 4 == 0, "groups of 4 slots");
     float pt0 = ta, pt1 = tb;
     uint32_t pp0 = pk, pp1 = pk;
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-        const bool c0 = pt0 < kt[i];
-        const float st = kt[i];
-        const uint32_t sp = kp[i];
-        kt[i] = c0 ? pt0 : st;
-        kp[i] = c0 ? pp0 : sp;
-        const float xt = c0 ? st : pt0;
-        const uint32_t xp = c0 ? sp : pp0;
-        const bool c1 = pt1 < xt;
-        pt0 = c1 ? pt1 : xt;
-        pp0 = c1 ? pp1 : xp;
-        pt1 = c1 ? xt : pt1;
-        pp1 = c1 ? xp : pp1;
+    for (int g = 0; g < K; g += 4) {
+        if (__builtin_amdgcn_ballot_w64(pt0 < kt[g + 3])) {
+#pragma unroll
+            for (int i = g; i < g + 4; ++i) {
+                const bool c0 = pt0 < kt[i];
+                const float st = kt[i];
+                const uint32_t sp = kp[i];
+                kt[i] = c0 ? pt0 : st;
+                kp[i] = c0 ? pp0 : sp;
+                const float xt = c0 ? st : pt0;
+                const uint32_t xp = c0 ? sp : pp0;
+                const bool c1 = pt1 < xt;
+                pt0 = c1 ? pt1 : xt;
+                pp0 = c1 ? pp1 : xp;
+                pt1 = c1 ? xt : pt1;
+                pp1 = c1 ? xp : pp1;
+            }
+        }
     }
 }
 
@@ -210,26 +217,47 @@ __device__ inline bool particle_alpha(f3 ok, f3 dk, float l2, float density, flo
 // centre m = -(n . ok) / (n . dk) +- hk / |n . dk|; the reciprocal is clamped to +-1e30 so a ray
 // parallel to a slab gives an unbounded interval when inside it and an empty one when outside.
 __device__ inline void ico_clip(f3 ok, f3 dk, float hk, float& tn, float& tf) {
-    // n . ok and n . dk for the 10 normals, sharing partial sums
-    const float pxy = ok.x + ok.y, mxy = ok.x - ok.y, qxy = dk.x + dk.y, nxy = dk.x - dk.y;
-    const float px = PHI * ok.x, py = PHI * ok.y, pz = PHI * ok.z;
-    const float qx = PHI * dk.x, qy = PHI * dk.y, qz = PHI * dk.z;
-    const float sa[10] = {pxy + ok.z, pxy - ok.z, mxy + ok.z, ok.z - mxy,
-                          fmaf(IPHI, ok.z, py), fmaf(-IPHI, ok.z, py), fmaf(IPHI, ok.x, pz), fmaf(-IPHI, ok.x, pz),
-                          fmaf(IPHI, ok.y, px), fmaf(-IPHI, ok.y, px)};
-    const float sb[10] = {qxy + dk.z, qxy - dk.z, nxy + dk.z, dk.z - nxy,
-                          fmaf(IPHI, dk.z, qy), fmaf(-IPHI, dk.z, qy), fmaf(IPHI, dk.x, qz), fmaf(-IPHI, dk.x, qz),
-                          fmaf(IPHI, dk.y, qx), fmaf(-IPHI, dk.y, qx)};
     float lo = -INFINITY, hi = INFINITY;
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-        const float ib = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(sb[i]), -1e30f, 1e30f);
+    // one slab at a time (short live ranges: this runs with the whole k-buffer in registers)
+    auto slab = [&](float sa, float sb) {
+        const float ib = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(sb), -1e30f, 1e30f);
         const float h = hk * fabsf(ib);
-        lo = fmaxf(lo, fmaf(-sa[i], ib, -h));
-        hi = fminf(hi, fmaf(-sa[i], ib, h));
+        lo = fmaxf(lo, fmaf(-sa, ib, -h));
+        hi = fminf(hi, fmaf(-sa, ib, h));
+    };
+    {
+        const float pxy = ok.x + ok.y, qxy = dk.x + dk.y;
+        slab(pxy + ok.z, qxy + dk.z);
+        slab(pxy - ok.z, qxy - dk.z);
+    }
+    {
+        const float mxy = ok.x - ok.y, nxy = dk.x - dk.y;
+        slab(mxy + ok.z, nxy + dk.z);
+        slab(ok.z - mxy, dk.z - nxy);
+    }
+    {
+        const float py = PHI * ok.y, qy = PHI * dk.y;
+        slab(fmaf(IPHI, ok.z, py), fmaf(IPHI, dk.z, qy));
+        slab(fmaf(-IPHI, ok.z, py), fmaf(-IPHI, dk.z, qy));
+    }
+    {
+        const float pz = PHI * ok.z, qz = PHI * dk.z;
+        slab(fmaf(IPHI, ok.x, pz), fmaf(IPHI, dk.x, qz));
+        slab(fmaf(-IPHI, ok.x, pz), fmaf(-IPHI, dk.x, qz));
+    }
+    {
+        const float px = PHI * ok.x, qx = PHI * dk.x;
+        slab(fmaf(IPHI, ok.y, px), fmaf(IPHI, dk.y, qx));
+        slab(fmaf(-IPHI, ok.y, px), fmaf(-IPHI, dk.y, qx));
     }
     tn = lo;
     tf = hi;
+}
+
+__device__ inline int32_t writelane(int32_t old, int32_t v, int32_t lane) {
+    // gfx9 constant-bus rule: with an SGPR source the lane select must come from M0
+    asm("v_writelane_b32 %0, %1, m0" : "+v"(old) : "s"(v), "{m0}"(lane));  // not volatile: no memory effects
+    return old;
 }
 
 __device__ inline uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -249,10 +277,16 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                                                 uint8_t* __restrict__ rgba8_, float* __restrict__ rgba32f_,
                                                 float* __restrict__ ray_dirs_, uint32_t* __restrict__ hit_counts_,
                                                 unsigned long long* __restrict__ stats_) {
-    __shared__ int32_t s_stack[4][STACK_DEPTH];
     // SH basis of each lane's ray direction, chunk-major so one ds_read_b128 per chunk is
     // conflict-free (16 KB per block; occupancy is VGPR-bound, not LDS-bound)
     __shared__ float4 s_basis[4][4][64];
+    // composite state (rgb, alpha accumulator) and transmittance, parked in LDS during traversal so
+    // their VGPRs go to the k-buffer (2 x KB registers)
+    __shared__ float4 s_acc[4][64];
+    __shared__ float s_T[4][64];
+#if !GVRT_VSTACK
+    __shared__ int32_t s_stack[4][STACK_DEPTH];
+#endif
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const uint64_t tile_idx = (uint64_t)blockIdx.x * 4 + wid;
@@ -307,18 +341,40 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
     }
     const float term_cut = a.min_transmittance * 0.9999f;
     float last = fmaxf(0.0f, tminb - EPS_T);
-    float T = 1.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f, calpha = a.alpha_init;
+    s_acc[wid][lane] = make_float4(0.0f, 0.0f, 0.0f, a.alpha_init);
+    s_T[wid][lane] = 1.0f;
     // counters: only the STATS instantiation keeps them (registers); the accepted-hit count is
     // recovered exactly from the alpha accumulator (RQ/RT alpha = alpha_init + #accepted, Q10)
     uint32_t nproc = 0, rounds = 0;
     uint32_t w_nodes = 0, w_leaves = 0, l_leaves = 0;  // wave node visits, wave leaf visits, lane leaf tests
-    bool active = valid && a.nrecs > 0 && (last <= tmaxb) && (T > a.min_transmittance);
+    bool active = valid && a.nrecs > 0 && (last <= tmaxb) && (1.0f > a.min_transmittance);
 
     static_assert(!(LITERAL && PACK), "LITERAL keeps rejected crossings: unpacked k-buffer");
     float kt[KB];
     uint32_t kid[KB];       // record id, or the packed payload (id << 8 | q) when PACK
     float ka[PACK ? 1 : KB];  // alpha per slot (unpacked only; < 0 = rejected crossing in LITERAL)
+#if GVRT_VSTACK
+    // Per-wave traversal stack in two VGPRs, entry i in lane i & 63 of stk[i >> 6] (v_writelane /
+    // v_readlane with a uniform index: no LDS round trip on a pop)
+    static_assert(STACK_DEPTH == 128, "two VGPRs of 64 lanes");
+    int32_t stk0 = 0, stk1 = 0;
+    int sp = 0;
+    auto push = [&](int32_t v) {
+        if (sp < 64) stk0 = writelane(stk0, v, sp);
+        else stk1 = writelane(stk1, v, sp - 64);
+        ++sp;
+    };
+    auto pop = [&]() -> int32_t {
+        --sp;
+        return sp < 64 ? __builtin_amdgcn_readlane(stk0, sp) : __builtin_amdgcn_readlane(stk1, sp - 64);
+    };
+#else
+    // Per-wave traversal stack in LDS
     int32_t* stack = s_stack[wid];
+    int sp = 0;
+    auto push = [&](int32_t v) { stack[sp++] = v; };
+    auto pop = [&]() -> int32_t { return unii(stack[--sp]); };
+#endif
     {
         // radianceFromSpH basis factors (gaussianfunctions.glsl:122-151), signs folded, zero past
         // sph_eval_degree; computed once per ray and kept in LDS (not registers) through the traversal
@@ -359,14 +415,15 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
         // drives T below minTransmittance (q sums never exceed the exact depth; +0.5 q of margin)
         uint32_t qneed = 0;
         if constexpr (PACK) {
-            const float need = T > term_cut ? __log2f(T / term_cut) * QSCALE + 0.5f : 0.0f;
+            const float Tr = s_T[wid][lane];
+            const float need = Tr > term_cut ? __log2f(Tr / term_cut) * QSCALE + 0.5f : 0.0f;
             qneed = (uint32_t)fminf(ceilf(need), 4.0e9f);
         }
 
         // ---------------- trace(): packet traversal of the 4-wide LBVH
         float tcut = INF_DIST;  // termination-aware cull distance of this lane (see the leaf insert)
         const uint64_t amask = __builtin_amdgcn_ballot_w64(active);
-        int sp = 0;
+        sp = 0;
         Bvh4Node nd = nodes_[0];  // whole node: 2x s_load_dwordx16
         while (true) {
             if constexpr (STATS) ++w_nodes;
@@ -389,8 +446,10 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
             }
             leafmask = uni(leafmask);
 
-            // ---- choose the next node before the leaf work (all on uniform values: SALU)
-            uint32_t key[4];  // entry distance bits: distances are >= tlo > 0, so uint order = float order
+            // ---- choose the next node before the leaf work (uniform values: SALU).  Key = entry
+            // distance of the first lane that hits the child; distances are >= tlo > 0, so uint
+            // order = float order.  (A branch-free form of this block measured 8 % slower.)
+            uint32_t key[4];
             int32_t cid[4];
             int nint = 0;
 #pragma unroll
@@ -398,7 +457,6 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                 key[k] = 0xFFFFFFFFu;
                 cid[k] = -1;
                 if (bal[k] && ch[k] >= 0) {
-                    // nearest first by the entry distance of the first lane that hits the child
                     key[k] = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(ent[k]), (int)__builtin_ctzll(bal[k]));
                     cid[k] = ch[k];
                     ++nint;
@@ -406,7 +464,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
             }
             int32_t next = -1;
             if (nint > 0) {
-                // sort the (key, child) pairs ascending: 5-comparator network on uniform values
+                // sort the (key, child) pairs ascending: 5-comparator network
 #define GVRT_CX(i, j)                                          \
     {                                                          \
         const bool sw = key[j] < key[i];                       \
@@ -419,41 +477,22 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
     }
                 GVRT_CX(0, 1) GVRT_CX(2, 3) GVRT_CX(0, 2) GVRT_CX(1, 3) GVRT_CX(1, 2)
 #undef GVRT_CX
-                for (int k = nint - 1; k >= 1; --k) {
-                    stack[sp] = cid[k];
-                    ++sp;
-                }
+                // farther children on the stack, the second-nearest on top
+                for (int k = nint - 1; k >= 1; --k) push(cid[k]);
                 next = unii(cid[0]);
             } else if (sp > 0) {
-                --sp;
-                next = unii(stack[sp]);
+                next = pop();
             }
-#if GVRT_NODE_PREFETCH
-            Bvh4Node nd_next;
-            if (next >= 0) nd_next = nodes_[next];
-#endif
 
             // ---- leaves of this node (the k-buffer orders them); one rolled loop = one insertion
             // site; the next leaf's record load is issued before the current leaf's tests
-#if GVRT_PREFETCH
-            RenderRec rec_next;
-            if (leafmask) rec_next = recs_[~ch[__builtin_ctz(leafmask)]];
-#endif
 #pragma unroll 1
             while (leafmask) {
                 const int k = __builtin_ctz(leafmask);
                 leafmask &= leafmask - 1;
                 const uint64_t bk = k == 0 ? bal[0] : (k == 1 ? bal[1] : (k == 2 ? bal[2] : bal[3]));
                 const int32_t ck = k == 0 ? ch[0] : (k == 1 ? ch[1] : (k == 2 ? ch[2] : ch[3]));
-#if GVRT_PREFETCH
-                const RenderRec rec = rec_next;
-                if (leafmask) {
-                    const int kn = __builtin_ctz(leafmask);
-                    rec_next = recs_[~(kn == 0 ? ch[0] : (kn == 1 ? ch[1] : (kn == 2 ? ch[2] : ch[3])))];
-                }
-#else
                 const RenderRec rec = recs_[~ck];
-#endif
                 {
                     const uint32_t gi = uni((uint32_t)(~ck));
                     if constexpr (STATS) ++w_leaves;
@@ -502,7 +541,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                                     // is the last one that can ever be composited (the loop ends there), so
                                     // nothing farther is needed.  The 1e-4 margin keeps the bound
                                     // conservative against ulp differences from the composite's arithmetic.
-                                    float Tp = T, tt = INF_DIST;
+                                    float Tp = s_T[wid][lane], tt = INF_DIST;
 #pragma unroll
                                     for (int i = 0; i < KB; ++i) {
                                         const bool acc_i = kid[i] != INVALID_ID && ka[i] > 0.0f;
@@ -518,11 +557,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                 }
             }
             if (next < 0) break;
-#if GVRT_NODE_PREFETCH
-            nd = nd_next;
-#else
-            nd = nodes_[next];
-#endif
+            nd = nodes_[unii(next)];  // uniform by construction; readfirstlane lets the compiler see it
         }
 
         // ---------------- process k hits (particleRendering.comp:153-187)
@@ -530,6 +565,8 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
             if (kid[0] == INVALID_ID) {
                 active = false;
             } else {
+                float T = s_T[wid][lane];
+                float4 acc = s_acc[wid][lane];
                 // rolled loop over slots: composite slot 0, then shift the buffer down by one
 #pragma unroll 1
                 for (int it = 0; it < KB; ++it) {
@@ -572,10 +609,10 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                             rr = fmaxf(rr + 0.5f, 0.0f);
                             rg = fmaxf(rg + 0.5f, 0.0f);
                             rb = fmaxf(rb + 0.5f, 0.0f);
-                            cr += rr * weight;
-                            cg += rg * weight;
-                            cb += rb * weight;
-                            calpha += 1.0f;
+                            acc.x += rr * weight;
+                            acc.y += rg * weight;
+                            acc.z += rb * weight;
+                            acc.w += 1.0f;
                             T *= (1.0f - halpha);
                         }
                         last = fmaxf(last, kt[0]);
@@ -589,11 +626,15 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                     kid[KB - 1] = INVALID_ID;
                 }
                 active = (last <= tmaxb) && (T > a.min_transmittance);
+                s_T[wid][lane] = T;
+                s_acc[wid][lane] = acc;
             }
         }
     }
 
     // ---------------- outputs
+    const float4 acc = s_acc[wid][lane];
+    const float cr = acc.x, cg = acc.y, cb = acc.z, calpha = acc.w;
     if (valid) {
         const uint64_t pix = ((uint64_t)cam * a.height + py) * a.width + px;
         const uint64_t oi = a.packed ? tile_idx * 64 + lane : pix;
@@ -672,13 +713,16 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
         if (adaptive) GVRT_LAUNCH(false, true, K_HITS, false);
         else GVRT_LAUNCH(false, false, K_HITS, false);
     } else if (adaptive) {
-        GVRT_LAUNCH(false, true, K_HITS, true);
+        GVRT_LAUNCH(false, true, K_FAST_DEFAULT, true);
     } else {
         // FAST: the k-buffer depth only sets the number of traversal rounds, not the image
         switch (a.kfast) {
             case 8: GVRT_LAUNCH(false, false, 8, true); break;
             case 12: GVRT_LAUNCH(false, false, 12, true); break;
-            default: GVRT_LAUNCH(false, false, K_HITS, true); break;
+            case 16: GVRT_LAUNCH(false, false, 16, true); break;
+            case 20: GVRT_LAUNCH(false, false, 20, true); break;
+            case 32: GVRT_LAUNCH(false, false, 32, true); break;
+            default: GVRT_LAUNCH(false, false, K_FAST_DEFAULT, true); break;
         }
     }
 #undef GVRT_LAUNCH
