@@ -48,6 +48,9 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 #ifndef GVRT_FMA_BOX
 #define GVRT_FMA_BOX 1
 #endif
+#ifndef GVRT_TCUT
+#define GVRT_TCUT 1
+#endif
 #ifndef GVRT_VSTACK
 #define GVRT_VSTACK 0
 #endif
@@ -419,6 +422,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
             const float need = Tr > term_cut ? __log2f(Tr / term_cut) * QSCALE + 0.5f : 0.0f;
             qneed = (uint32_t)fminf(ceilf(need), 4.0e9f);
         }
+        uint32_t qtot = 0;  // PACK: sum of the q codes inserted this round (>= the buffer's sum)
 
         // ---------------- trace(): packet traversal of the 4-wide LBVH
         float tcut = INF_DIST;  // termination-aware cull distance of this lane (see the leaf insert)
@@ -523,9 +527,14 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                                 const float tb = (in0 && in1 && tf < tcut) ? tf : INF_DIST;
                                 if (ta < kt[KB - 1]) {
                                   if constexpr (PACK) {
-                                    kb_insert2p<KB>(ta, tb, (gi << 8) | alpha_code(galpha), kt, kid);
+                                    const uint32_t q = alpha_code(galpha);
+                                    kb_insert2p<KB>(ta, tb, (gi << 8) | q, kt, kid);
                                     // termination cull on the q codes (see kb_insert2p): the first slot
-                                    // whose running sum reaches qneed is the last one composited
+                                    // whose running sum reaches qneed is the last one composited; no
+                                    // slot can reach it while the inserted total is still below
+                                    qtot += tb < INF_DIST ? 2 * q : q;
+#if GVRT_TCUT
+                                    if (__builtin_amdgcn_ballot_w64(qtot >= qneed)) {
                                     uint32_t qs = 0;
                                     float tt = INF_DIST;
 #pragma unroll
@@ -534,6 +543,8 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                                         tt = fminf(tt, qs >= qneed ? kt[i] : INF_DIST);
                                     }
                                     tcut = fminf(tcut, tt);
+                                    }
+#endif
                                   } else {
                                     kb_insert2<KB>(ta, tb, gi, al, kt, kid, ka);
                                     // Termination-aware cull distance: walking the sorted slots with the
