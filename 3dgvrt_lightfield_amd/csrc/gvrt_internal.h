@@ -48,7 +48,8 @@ struct gvrt_context {
     gvrt::Bvh4Node* d_nodes4 = nullptr; // 4-wide collapse traversed by the render kernel
     uint64_t n_nodes4 = 0;
     uint32_t* d_leaf_src = nullptr;  // leaf -> compaction index
-    uint32_t depth = 0;
+    uint32_t depth = 0;   // binary LBVH depth
+    uint32_t depth4 = 0;  // 4-wide levels (bounds the traversal stack: 3 pushes per level)
 
     // per-render scratch
     bool stats_on = false;

@@ -267,6 +267,81 @@ __global__ __launch_bounds__(256) void k_collapse(int64_t ni, const BvhNode* __r
     out[idx4[i]] = o;
 }
 
+__device__ inline float half_area(const float* b) {
+    const float ex = b[3] - b[0], ey = b[4] - b[1], ez = b[5] - b[2];
+    return ex * ey + ey * ez + ez * ex;
+}
+
+// Greedy surface-area collapse, one 4-wide level per launch (ctl = {begin, end, allocated, depth}):
+// a 4-wide node starts from its binary root's two children and opens the internal child with the
+// largest surface area until it holds four; its internal children become next-level 4-wide nodes
+// (ids allocated contiguously per level, so each level is one contiguous, breadth-first range).
+__global__ __launch_bounds__(256) void k_collapse_level(const BvhNode* __restrict__ bin, int32_t* __restrict__ src4,
+                                                        uint32_t* __restrict__ ctl, uint32_t level,
+                                                        Bvh4Node* __restrict__ out) {
+    const uint32_t begin = ctl[0], end = ctl[1];
+    const uint64_t i = (uint64_t)begin + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= end) return;
+    const BvhNode n = bin[src4[i]];
+    int32_t ref[4];
+    float box[4][6];
+    const float* nb = reinterpret_cast<const float*>(&n);
+    ref[0] = n.c0;
+    ref[1] = n.c1;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        box[0][k] = nb[k];
+        box[1][k] = nb[6 + k];
+    }
+    int cnt = 2;
+    while (cnt < 4) {
+        int best = -1;
+        float ba = -1.0f;
+        for (int j = 0; j < cnt; ++j) {
+            if (ref[j] >= 0) {
+                const float ar = half_area(box[j]);
+                if (ar > ba) {
+                    ba = ar;
+                    best = j;
+                }
+            }
+        }
+        if (best < 0) break;
+        const BvhNode g = bin[ref[best]];
+        const float* gb = reinterpret_cast<const float*>(&g);
+        ref[best] = g.c0;
+        ref[cnt] = g.c1;
+        for (int k = 0; k < 6; ++k) {
+            box[best][k] = gb[k];
+            box[cnt][k] = gb[6 + k];
+        }
+        ++cnt;
+    }
+    Bvh4Node o;
+    bool inner = false;
+    for (int j = 0; j < cnt; ++j) {
+        int32_t r = ref[j];
+        if (r >= 0) {
+            const uint32_t id = atomicAdd(ctl + 2, 1u);
+            src4[id] = r;
+            r = (int32_t)id;
+            inner = true;
+        }
+        put_slot(o, j, box[j], r);
+    }
+    const float eb[6] = {EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX};
+    o.nchild = (uint32_t)cnt;
+    for (int j = cnt; j < 4; ++j) put_slot(o, j, eb, 0);
+    o.pad[0] = o.pad[1] = o.pad[2] = 0;
+    out[i] = o;
+    if (inner) atomicMax(ctl + 3, level + 1);
+}
+
+__global__ void k_level_advance(uint32_t* ctl) {
+    ctl[0] = ctl[1];
+    ctl[1] = ctl[2];
+}
+
 }  // namespace
 
 gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
@@ -333,7 +408,7 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
     TRY(gvrt_dalloc(c, (void**)&keys2, 8ull * m));
     TRY(gvrt_dalloc(c, (void**)&vals2, 4ull * m));
     TRY(gvrt_dalloc(c, (void**)&counters, 4ull * ninternal));
-    TRY(gvrt_dalloc(c, (void**)&dep, 16));
+    TRY(gvrt_dalloc(c, (void**)&dep, 32));
     TRY(gvrt_dalloc(c, (void**)&lpar, 4ull * m));
     TRY(gvrt_dalloc(c, (void**)&npar, 4ull * ninternal));
     TRY(gvrt_dalloc(c, (void**)&lboxes, 24ull * m));
@@ -372,6 +447,7 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
         TRYH(hipMemcpyAsync(c->d_nodes4, &root, sizeof(root), hipMemcpyHostToDevice, c->stream), "root");
         c->n_nodes4 = 1;
         c->depth = 1;
+        c->depth4 = 1;
     } else {
         TRYH(hipMemsetAsync(counters, 0, 4ull * ninternal, c->stream), "memset");
         TRYH(hipMemsetAsync(dep, 0, 4, c->stream), "memset");
@@ -382,8 +458,35 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
         TRYH(hipGetLastError(), "k_karras/k_refit");
         uint32_t hd = 0;
         TRYH(hipMemcpyAsync(&hd, dep, 4, hipMemcpyDeviceToHost, c->stream), "depth");
-        // ---- collapse to the 4-wide tree (reuse keys/vals as flags / scan)
         const int64_t ni = m - 1;
+        const char* ce = getenv("GVRT_COLLAPSE");
+        const bool greedy = !(ce && ce[0] == '0');
+        if (greedy) {
+            // ---- greedy surface-area collapse, level by level (upper bound: one 4-wide node per binary node)
+            int32_t* src4 = lpar;  // lpar (m entries) is free after k_depth
+            uint32_t* ctl = dep + 4;  // dep: [0] depth census, [4..7] collapse control
+            const uint32_t ctl0[4] = {0u, 1u, 1u, 0u};
+            TRYH(hipMemcpyAsync(ctl, ctl0, 16, hipMemcpyHostToDevice, c->stream), "ctl");
+            TRYH(hipMemsetAsync(src4, 0, 4, c->stream), "src4");
+            TRY(gvrt_dalloc(c, (void**)&c->d_nodes4, sizeof(Bvh4Node) * ni));
+            TRYH(hipStreamSynchronize(c->stream), "sync");  // hd (binary depth) bounds the level count
+            uint64_t width = 1;
+            for (uint32_t lv = 0; lv <= hd; ++lv) {
+                const uint64_t w = width < (uint64_t)ni ? width : (uint64_t)ni;
+                hipLaunchKernelGGL(k_collapse_level, dim3((unsigned)((w + 255) / 256)), dim3(256), 0, c->stream, c->d_nodes,
+                                   src4, ctl, lv, c->d_nodes4);
+                hipLaunchKernelGGL(k_level_advance, dim3(1), dim3(1), 0, c->stream, ctl);
+                width = width * 4 < (uint64_t)ni ? width * 4 : (uint64_t)ni;
+            }
+            TRYH(hipGetLastError(), "k_collapse_level");
+            uint32_t hc[4];
+            TRYH(hipMemcpyAsync(hc, ctl, 16, hipMemcpyDeviceToHost, c->stream), "ctl");
+            TRYH(hipStreamSynchronize(c->stream), "sync");
+            c->depth = hd;
+            c->depth4 = hc[3] + 1;
+            c->n_nodes4 = hc[2];
+        } else {
+        // ---- collapse to the 4-wide tree by even depth (reuse keys/vals as flags / scan)
         uint32_t* flags = reinterpret_cast<uint32_t*>(keys);
         hipLaunchKernelGGL(k_even_flags, dim3((unsigned)((ni + 1 + 255) / 256)), dim3(256), 0, c->stream, ni, npar,
                            flags);
@@ -399,11 +502,13 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
         TRYH(hipMemcpyAsync(&n4, vals + ni, 4, hipMemcpyDeviceToHost, c->stream), "n4");
         TRYH(hipStreamSynchronize(c->stream), "sync");
         c->depth = hd;
+        c->depth4 = (hd + 1) / 2 + 1;
         TRY(gvrt_dalloc(c, (void**)&c->d_nodes4, sizeof(Bvh4Node) * (n4 ? n4 : 1)));
         hipLaunchKernelGGL(k_collapse, dim3((unsigned)((ni + 255) / 256)), dim3(256), 0, c->stream, ni, c->d_nodes,
                            flags, vals, c->d_nodes4);
         TRYH(hipGetLastError(), "k_collapse");
         c->n_nodes4 = n4;
+        }
     }
     TRYH(hipEventRecord(c->ev1, c->stream), "event");
     TRYH(hipStreamSynchronize(c->stream), "sync");
@@ -414,7 +519,7 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
 #undef TRY
 #undef TRYH
     // the 4-wide traversal pushes at most 3 entries per 4-wide level
-    if (3 * ((c->depth + 1) / 2) + 2 > (uint32_t)STACK_DEPTH)
+    if (3 * c->depth4 + 2 > (uint32_t)STACK_DEPTH)
         return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "LBVH deeper than the render kernel's traversal stack");
     c->stats.bvh_nodes = c->n_nodes4;
     c->stats.bvh_depth = c->depth;
