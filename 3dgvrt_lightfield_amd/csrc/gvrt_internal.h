@@ -79,6 +79,8 @@ void gvrt_dfree(gvrt_context* c, void** p);
 gvrt_status gvrt_launch_enclose(gvrt_context* c, const gvrt_enclosing_params* p, uint64_t* m);
 // gvrt_lbvh.hip
 gvrt_status gvrt_launch_build_accel(gvrt_context* c);
+gvrt_status gvrt_ploc_build(gvrt_context* c, uint32_t m, const float* leaf_boxes, gvrt::BvhNode* bin,
+                            int32_t* leaf_parent, int32_t* node_parent, int32_t* root, uint32_t* iterations);
 // gvrt_render.hip
 gvrt_status gvrt_launch_render_mode(gvrt_context* c, const gvrt::RenderArgs& a, uint64_t nwaves, bool literal);
 gvrt_status gvrt_launch_unpack(gvrt_context* c, const void* packed, const uint32_t* tiles,

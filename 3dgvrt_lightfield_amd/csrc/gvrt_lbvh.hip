@@ -451,23 +451,31 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
     } else {
         TRYH(hipMemsetAsync(counters, 0, 4ull * ninternal, c->stream), "memset");
         TRYH(hipMemsetAsync(dep, 0, 4, c->stream), "memset");
-        const unsigned iblocks = (unsigned)((m - 1 + 255) / 256);
-        hipLaunchKernelGGL(k_karras, dim3(iblocks), dim3(256), 0, c->stream, m, keys2, c->d_nodes, lpar, npar);
-        hipLaunchKernelGGL(k_refit, dim3(blocks), dim3(256), 0, c->stream, m, lboxes, c->d_nodes, lpar, npar, counters);
+        const char* be = getenv("GVRT_BUILDER");
+        const bool ploc = be && be[0] == 'p';  // "ploc": measured 3 % slower to render (more visits), see DESIGN.md
+        int32_t root = 0;
+        if (ploc) {
+            uint32_t iters = 0;
+            TRY(gvrt_ploc_build(c, (uint32_t)m, lboxes, c->d_nodes, lpar, npar, &root, &iters));
+        } else {
+            const unsigned iblocks = (unsigned)((m - 1 + 255) / 256);
+            hipLaunchKernelGGL(k_karras, dim3(iblocks), dim3(256), 0, c->stream, m, keys2, c->d_nodes, lpar, npar);
+            hipLaunchKernelGGL(k_refit, dim3(blocks), dim3(256), 0, c->stream, m, lboxes, c->d_nodes, lpar, npar, counters);
+        }
         hipLaunchKernelGGL(k_depth, dim3(blocks), dim3(256), 0, c->stream, m, lpar, npar, dep);
         TRYH(hipGetLastError(), "k_karras/k_refit");
         uint32_t hd = 0;
         TRYH(hipMemcpyAsync(&hd, dep, 4, hipMemcpyDeviceToHost, c->stream), "depth");
         const int64_t ni = m - 1;
         const char* ce = getenv("GVRT_COLLAPSE");
-        const bool greedy = !(ce && ce[0] == '0');
+        const bool greedy = ploc || !(ce && ce[0] == '0');  // the even-depth rule needs the Karras layout
         if (greedy) {
             // ---- greedy surface-area collapse, level by level (upper bound: one 4-wide node per binary node)
             int32_t* src4 = lpar;  // lpar (m entries) is free after k_depth
             uint32_t* ctl = dep + 4;  // dep: [0] depth census, [4..7] collapse control
             const uint32_t ctl0[4] = {0u, 1u, 1u, 0u};
             TRYH(hipMemcpyAsync(ctl, ctl0, 16, hipMemcpyHostToDevice, c->stream), "ctl");
-            TRYH(hipMemsetAsync(src4, 0, 4, c->stream), "src4");
+            TRYH(hipMemcpyAsync(src4, &root, 4, hipMemcpyHostToDevice, c->stream), "src4");
             TRY(gvrt_dalloc(c, (void**)&c->d_nodes4, sizeof(Bvh4Node) * ni));
             TRYH(hipStreamSynchronize(c->stream), "sync");  // hd (binary depth) bounds the level count
             uint64_t width = 1;
