@@ -314,6 +314,8 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
 #endif
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
+    // (Round-robin workgroup -> XCD dealing is kept: an XCD-contiguous band remap measured 33 % slower,
+    // the bands' very different costs leave a long tail; L2 hit rate is already ~91 %.)
     const uint64_t tile_idx = (uint64_t)blockIdx.x * 4 + wid;
     if (tile_idx >= a.ntiles) return;  // wave-uniform
     uint32_t cam, tx, ty;
