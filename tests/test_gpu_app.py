@@ -1,0 +1,60 @@
+"""The headless app (3dgvrt_lightfield_amd/app.py) end to end on the GPU: PLY -> prepare -> eval capture
+(r_<i>.png per NeRF camera), light-field batch (PNG per view + rayDirs), hit-count dump, fps.txt."""
+import importlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+app = importlib.import_module("3dgvrt_lightfield_amd.app")
+
+
+def test_app_eval_lightfield_hitcounts_bench(gv, tmp_path):
+    pytest.importorskip("PIL")
+    splats = gv.scene.config1(n=2000)
+    ply = str(tmp_path / "scene.ply")
+    gv.save_ply(ply, splats)
+    # a NeRF transforms file with two cameras on a circle, looking at the origin
+    frames = []
+    for a in (0.0, 0.7):
+        eye = np.array([3 * np.sin(a), 0.0, 3 * np.cos(a)])
+        f = -eye / np.linalg.norm(eye)
+        r = np.cross(f, [0.0, 1.0, 0.0]); r /= np.linalg.norm(r)
+        u = np.cross(r, f)
+        c2w = np.eye(4); c2w[:3, 0], c2w[:3, 1], c2w[:3, 2], c2w[:3, 3] = r, u, -f, eye
+        frames.append({"file_path": "./val/r_x", "transform_matrix": c2w.tolist()})
+    tj = tmp_path / "transforms_val.json"
+    tj.write_text(json.dumps({"camera_angle_x": 0.69, "frames": frames}))
+
+    with app.GvrtApp(0) as a:
+        m = a.prepare(ply=ply)
+        assert m > 0
+        out = tmp_path / "eval"
+        assert a.eval_capture(str(tj), str(out), 64, 64) == 2
+        r0 = app.load_png_rgb(str(out / "r_0.png"))
+        # the PNG is exactly the frame draw() returns for that camera
+        _, views = gv.camera.load_nerf_cameras(str(tj))
+        import math
+        proj = gv.camera.perspective_vulkan_no_depth_reverse(math.radians(gv.camera.FOV_Y), 1.0, gv.camera.NEAR_PLANE,
+                                                             gv.camera.FAR_PLANE)
+        img = a.draw(gv.camera.colmajor(gv.camera.inverse(views[0])), gv.camera.colmajor(gv.camera.inverse(proj)), 64, 64,
+                     rgba32f=False)["rgba8"][0]
+        np.testing.assert_array_equal(r0, img[..., :3])
+        assert img[..., 3].max() > 0  # the camera sees the scene
+
+        lf = tmp_path / "lf"
+        assert a.light_field(str(lf), "ring", 48, 48) == 4
+        assert sorted(os.listdir(lf)) == ["rayDirs.npy", "view_0.png", "view_1.png", "view_2.png", "view_3.png"]
+        d = np.load(str(lf / "rayDirs.npy"))
+        assert d.shape == (4, 48, 48, 4)
+
+        vi, pi = gv.scene.config1_camera(32, 32)
+        hc = a.hit_counts(vi, pi, 32, 32, str(tmp_path / "rayHitCountsOutput.txt"))
+        rows = (tmp_path / "rayHitCountsOutput.txt").read_text().splitlines()
+        assert len(rows) == 32 and [int(v) for v in rows[5].split()] == hc[5].tolist()
+
+        fps, b = a.benchmark(vi, pi, 32, 32, warmup=0.05, duration=0.2, filename=str(tmp_path / "fps.txt"))
+        assert fps > 0
+        assert (tmp_path / "fps.txt").read_text().startswith("device,driverversion,duration (ms),frames,fps\n")
