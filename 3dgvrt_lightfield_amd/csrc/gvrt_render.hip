@@ -313,6 +313,8 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
     // their VGPRs go to the k-buffer (2 x KB registers)
     __shared__ float4 s_acc[4][64];
     __shared__ float s_T[4][64];
+    __shared__ float s_last[4][64];  // `last` and the AABB exit: round-boundary state, not needed in traversal
+    __shared__ float s_tmax[4][64];
 #if !GVRT_VSTACK
     __shared__ int32_t s_stack[4][STACK_DEPTH];
 #endif
@@ -371,14 +373,15 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
         tmaxb = fminf(fmaxf(t0x, t1x), fminf(fmaxf(t0y, t1y), fmaxf(t0z, t1z)));
     }
     const float term_cut = a.min_transmittance * 0.9999f;
-    float last = fmaxf(0.0f, tminb - EPS_T);
+    s_last[wid][lane] = fmaxf(0.0f, tminb - EPS_T);
+    s_tmax[wid][lane] = tmaxb;
     s_acc[wid][lane] = make_float4(0.0f, 0.0f, 0.0f, a.alpha_init);
     s_T[wid][lane] = 1.0f;
     // counters: only the STATS instantiation keeps them (registers); the accepted-hit count is
     // recovered exactly from the alpha accumulator (RQ/RT alpha = alpha_init + #accepted, Q10)
     uint32_t nproc = 0, rounds = 0;
     uint32_t w_nodes = 0, w_leaves = 0, l_leaves = 0;  // wave node visits, wave leaf visits, lane leaf tests
-    bool active = valid && a.nrecs > 0 && (last <= tmaxb) && (1.0f > a.min_transmittance);
+    bool active = valid && a.nrecs > 0 && (fmaxf(0.0f, tminb - EPS_T) <= tmaxb) && (1.0f > a.min_transmittance);
 
     static_assert(!(LITERAL && PACK), "LITERAL keeps rejected crossings: unpacked k-buffer");
     float kt[KB];
@@ -434,8 +437,8 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
         if constexpr (LITERAL || STATS) {
             if (active) ++rounds;
         }
-        const float tlo = last + EPS_T;
-        const float thi = tmaxb + EPS_T;
+        const float tlo = s_last[wid][lane] + EPS_T;
+        const float thi = s_tmax[wid][lane] + EPS_T;
 #pragma unroll
         for (int i = 0; i < KB; ++i) {
             kt[i] = INF_DIST;
@@ -540,7 +543,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                 {
                     const uint32_t gi = uni((uint32_t)(~ck));
                     if constexpr (STATS) ++w_leaves;
-                    if ((bk >> lane) & 1ull) {
+                    if (__builtin_amdgcn_inverse_ballot_w64(bk)) {  // exec &= bk: no per-lane bit test
                         if constexpr (STATS) ++l_leaves;
                         // ---- leaf: response (processHit's math) + analytic icosahedron clip
                         f3 ok, dk;
@@ -618,6 +621,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
             } else {
                 float T = s_T[wid][lane];
                 float4 acc = s_acc[wid][lane];
+                float last = s_last[wid][lane];
                 // rolled loop over slots: composite slot 0, then shift the buffer down by one
 #pragma unroll 1
                 for (int it = 0; it < KB; ++it) {
@@ -676,7 +680,8 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                     }
                     kid[KB - 1] = INVALID_ID;
                 }
-                active = (last <= tmaxb) && (T > a.min_transmittance);
+                active = (last <= s_tmax[wid][lane]) && (T > a.min_transmittance);
+                s_last[wid][lane] = last;
                 s_T[wid][lane] = T;
                 s_acc[wid][lane] = acc;
             }
