@@ -38,7 +38,7 @@ struct alignas(16) BvhNode {
     float h0y, h0z, l1x, l1y;
     float l1z, h1x, h1y, h1z;
     int32_t c0, c1;  // >= 0 internal node index; < 0 leaf ~index (record index)
-    uint32_t pad0, pad1;
+    uint32_t pad0, pad1;  // pad0: split axis (c0 on the lower side)
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 B");
 
@@ -51,7 +51,8 @@ struct alignas(16) Bvh4Node {
     float lox[4], loy[4], loz[4];
     float hix[4], hiy[4], hiz[4];
     int32_t child[4];  // >= 0: Bvh4Node index; < 0: leaf ~record index
-    uint32_t nchild, pad[3];
+    uint32_t nchild;
+    uint32_t pad[3];   // [0] split axis of the children's order (0 x, 1 y, 2 z), [1] internal-child mask
 };
 static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node must be 128 B");
 

@@ -156,7 +156,10 @@ __global__ __launch_bounds__(256) void k_karras(int64_t m, const uint64_t* __res
     }
     nodes[i].c0 = c0;
     nodes[i].c1 = c1;
-    nodes[i].pad0 = 0;
+    // split axis: the first Morton bit where the range differs (bit 3b+2 = x, 3b+1 = y, 3b = z); c0 is the
+    // lower side, so the render kernel can order children by the ray's direction on this axis
+    const int p = 63 - dnode;
+    nodes[i].pad0 = dnode >= 64 ? 0u : (uint32_t)(2 - p % 3);
     nodes[i].pad1 = 0;
     if (i == 0) node_parent[0] = -1;
 }
@@ -262,8 +265,12 @@ __global__ __launch_bounds__(256) void k_collapse(int64_t ni, const BvhNode* __r
     }
     const float eb[6] = {EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX};
     o.nchild = (uint32_t)k;
+    uint32_t imask = 0;
+    for (int j = 0; j < k; ++j) imask |= o.child[j] >= 0 ? (1u << j) : 0u;
     for (; k < 4; ++k) put_slot(o, k, eb, 0);
-    o.pad[0] = o.pad[1] = o.pad[2] = 0;
+    o.pad[0] = n.pad0;
+    o.pad[1] = imask;
+    o.pad[2] = 0;
     out[idx4[i]] = o;
 }
 
@@ -309,16 +316,21 @@ __global__ __launch_bounds__(256) void k_collapse_level(const BvhNode* __restric
         if (best < 0) break;
         const BvhNode g = bin[ref[best]];
         const float* gb = reinterpret_cast<const float*>(&g);
+        for (int j = cnt; j > best + 1; --j) {  // keep the children in order (c0 before c1)
+            ref[j] = ref[j - 1];
+            for (int k = 0; k < 6; ++k) box[j][k] = box[j - 1][k];
+        }
         ref[best] = g.c0;
-        ref[cnt] = g.c1;
+        ref[best + 1] = g.c1;
         for (int k = 0; k < 6; ++k) {
             box[best][k] = gb[k];
-            box[cnt][k] = gb[6 + k];
+            box[best + 1][k] = gb[6 + k];
         }
         ++cnt;
     }
     Bvh4Node o;
     bool inner = false;
+    uint32_t imask = 0;
     for (int j = 0; j < cnt; ++j) {
         int32_t r = ref[j];
         if (r >= 0) {
@@ -326,13 +338,16 @@ __global__ __launch_bounds__(256) void k_collapse_level(const BvhNode* __restric
             src4[id] = r;
             r = (int32_t)id;
             inner = true;
+            imask |= 1u << j;
         }
         put_slot(o, j, box[j], r);
     }
     const float eb[6] = {EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX};
     o.nchild = (uint32_t)cnt;
     for (int j = cnt; j < 4; ++j) put_slot(o, j, eb, 0);
-    o.pad[0] = o.pad[1] = o.pad[2] = 0;
+    o.pad[0] = n.pad0;  // split axis of the binary root (children are in its in-order)
+    o.pad[1] = imask;   // children that are 4-wide nodes
+    o.pad[2] = 0;
     out[i] = o;
     if (inner) atomicMax(ctl + 3, level + 1);
 }
@@ -443,6 +458,7 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
             root.child[k] = k == 0 ? ~0 : 0;
         }
         root.nchild = 1;
+        root.pad[0] = root.pad[1] = root.pad[2] = 0;
         TRY(gvrt_dalloc(c, (void**)&c->d_nodes4, sizeof(Bvh4Node)));
         TRYH(hipMemcpyAsync(c->d_nodes4, &root, sizeof(root), hipMemcpyHostToDevice, c->stream), "root");
         c->n_nodes4 = 1;

@@ -87,7 +87,11 @@ __global__ __launch_bounds__(256) void k_ploc_merge(uint32_t n, const int32_t* _
     const int32_t ri = refs[i], rj = refs[j];
     nd.c0 = ri;
     nd.c1 = rj;
-    nd.pad0 = nd.pad1 = 0;
+    // split axis (for the render kernel's child order): the axis of the largest centroid separation
+    float cs[3];
+    for (int k = 0; k < 3; ++k) cs[k] = fabsf((f[6 + k] + f[9 + k]) - (f[k] + f[3 + k]));
+    nd.pad0 = cs[0] >= cs[1] && cs[0] >= cs[2] ? 0u : (cs[1] >= cs[2] ? 1u : 2u);
+    nd.pad1 = 0;
     bin[id] = nd;
     if (ri < 0) leaf_parent[~ri] = (int32_t)id;
     else node_parent[ri] = (int32_t)id;

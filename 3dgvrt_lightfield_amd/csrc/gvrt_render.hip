@@ -48,8 +48,8 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 #ifndef GVRT_FMA_BOX
 #define GVRT_FMA_BOX 1
 #endif
-#ifndef GVRT_PK_BOX
-#define GVRT_PK_BOX 0
+#ifndef GVRT_ORDER
+#define GVRT_ORDER 0
 #endif
 #ifndef GVRT_TCUT
 #define GVRT_TCUT 1
@@ -80,25 +80,6 @@ __device__ inline bool box_hit(float lx, float ly, float lz, float hx, float hy,
     const float tf = fminf(fminf(t1, fmaxf(ax, bx)), fminf(fmaxf(ay, by), fmaxf(az, bz)));
     tenter = tn;
     return tn <= tf + 2e-6f * fabsf(tf);
-}
-
-// Two children per call with packed FP32 FMAs (v_pk_fma_f32: both children's plane distances in one
-// instruction; the SoA node puts each child pair's coordinates in adjacent SGPRs)
-typedef float pf2 __attribute__((ext_vector_type(2)));
-__device__ inline void box_hit2(pf2 lx, pf2 ly, pf2 lz, pf2 hx, pf2 hy, pf2 hz, f3 oinv, f3 inv, float t0, float t1,
-                                bool& h0, bool& h1, float& e0, float& e1) {
-    const pf2 ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
-    const pf2 nx = {-oinv.x, -oinv.x}, ny = {-oinv.y, -oinv.y}, nz = {-oinv.z, -oinv.z};
-    const pf2 ax = __builtin_elementwise_fma(lx, ix, nx), bx = __builtin_elementwise_fma(hx, ix, nx);
-    const pf2 ay = __builtin_elementwise_fma(ly, iy, ny), by = __builtin_elementwise_fma(hy, iy, ny);
-    const pf2 az = __builtin_elementwise_fma(lz, iz, nz), bz = __builtin_elementwise_fma(hz, iz, nz);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const float tn = fmaxf(fmaxf(t0, fminf(ax[j], bx[j])), fmaxf(fminf(ay[j], by[j]), fminf(az[j], bz[j])));
-        const float tf = fminf(fminf(t1, fmaxf(ax[j], bx[j])), fminf(fmaxf(ay[j], by[j]), fmaxf(az[j], bz[j])));
-        (j ? e1 : e0) = tn;
-        (j ? h1 : h0) = tn <= tf + 2e-6f * fabsf(tf);
-    }
 }
 
 template <int K>
@@ -362,7 +343,8 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
     const float dzs = fabsf(d.z) < 1e-12f ? copysignf(1e-12f, d.z) : d.z;
     const f3 inv = mk3(1.0f / dxs, 1.0f / dys, 1.0f / dzs);
     const f3 oinv = o * inv;
-
+    // direction signs of the wave's first ray (bit a: negative on axis a): child visiting order
+    [[maybe_unused]] const uint32_t rsign = uni((inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u));
     // intersectAABB (gaussianfunctions.glsl:8-16, Q12)
     float tminb, tmaxb;
     {
@@ -465,27 +447,47 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
             const float tc = fminf(fminf(thi, kt[KB - 1]), tcut);
             float ent[4];
             uint64_t bal[4];
-#if GVRT_PK_BOX
-#pragma unroll
-            for (int k = 0; k < 4; k += 2) {
-                bool h0, h1;
-                box_hit2(pf2{nd.lox[k], nd.lox[k + 1]}, pf2{nd.loy[k], nd.loy[k + 1]}, pf2{nd.loz[k], nd.loz[k + 1]},
-                         pf2{nd.hix[k], nd.hix[k + 1]}, pf2{nd.hiy[k], nd.hiy[k + 1]}, pf2{nd.hiz[k], nd.hiz[k + 1]},
-                         oinv, inv, tlo, tc, h0, h1, ent[k], ent[k + 1]);
-                bal[k] = __builtin_amdgcn_ballot_w64(h0) & amask;  // compare result straight to an SGPR mask
-                bal[k + 1] = __builtin_amdgcn_ballot_w64(h1) & amask;
-            }
-#else
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const bool hit = box_hit(nd.lox[k], nd.loy[k], nd.loz[k], nd.hix[k], nd.hiy[k], nd.hiz[k], o, oinv,
-                                         inv, tlo, tc, ent[k]);
-                bal[k] = __builtin_amdgcn_ballot_w64(hit) & amask;  // compare result straight to an SGPR mask
-            }
-#endif
+#define GVRT_BOX4(TEST)                                                                                 \
+    _Pragma("unroll") for (int k = 0; k < 4; ++k) {                                                     \
+        const bool hit = TEST(nd.lox[k], nd.loy[k], nd.loz[k], nd.hix[k], nd.hiy[k], nd.hiz[k], oinv, inv, \
+                              tlo, tc, ent[k]);                                                         \
+        bal[k] = __builtin_amdgcn_ballot_w64(hit) & amask; /* compare result straight to an SGPR mask */ \
+    }
+#define GVRT_BOX_GENERIC(lx, ly, lz, hx, hy, hz, oi, iv, t0, t1, e) box_hit(lx, ly, lz, hx, hy, hz, o, oi, iv, t0, t1, e)
+            // (a per-octant min/max-free box test was measured slower: 9 code copies, or its plane
+            // swaps moved to SALU — the scalar unit is on the critical path)
+            GVRT_BOX4(GVRT_BOX_GENERIC)
+#undef GVRT_BOX_GENERIC
+#undef GVRT_BOX4
             int32_t ch[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) ch[k] = unii(nd.child[k]);
+#if GVRT_ORDER == 0
+            // ---- children in the node's stored order (in-order of the binary split), forward when the
+            // first lane's ray points along +axis, else backward: a handful of SALU ops per node
+            // (the entry-distance sort below costs ~100)
+            uint32_t hm = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) hm |= bal[k] ? (1u << k) : 0u;
+            const uint32_t inner = uni(nd.pad[1]);
+            uint32_t leafmask = hm & ~inner;
+            uint32_t im = hm & inner;
+            int32_t next = -1;
+            auto chsel = [&](int k) { return k == 0 ? ch[0] : (k == 1 ? ch[1] : (k == 2 ? ch[2] : ch[3])); };
+            if (im) {
+                const bool rev = (rsign >> uni(nd.pad[0])) & 1u;
+                const int first = rev ? 31 - __clz(im) : __ffs(im) - 1;
+                next = chsel(first);
+                im &= ~(1u << first);
+                while (im) {  // the next child in visiting order ends on top
+                    const int k = rev ? __ffs(im) - 1 : 31 - __clz(im);
+                    push(chsel(k));
+                    im &= ~(1u << k);
+                }
+            } else if (sp > 0) {
+                next = pop();
+            }
+#else
             uint32_t leafmask = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -531,6 +533,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                 next = pop();
             }
 
+#endif
             // ---- leaves of this node (the k-buffer orders them); one rolled loop = one insertion
             // site; the next leaf's record load is issued before the current leaf's tests
 #pragma unroll 1
