@@ -84,13 +84,25 @@ __global__ __launch_bounds__(256) void k_ploc_merge(uint32_t n, const int32_t* _
         f[6 + k] = b;
         u[k] = k < 3 ? fminf(a, b) : fmaxf(a, b);
     }
-    const int32_t ri = refs[i], rj = refs[j];
+    int32_t ri = refs[i], rj = refs[j];
+    // split axis (for the render kernel's child order): the axis of the largest centroid separation,
+    // with c0 on its lower side
+    float cs[3];
+    for (int k = 0; k < 3; ++k) cs[k] = (f[6 + k] + f[9 + k]) - (f[k] + f[3 + k]);
+    const uint32_t ax = fabsf(cs[0]) >= fabsf(cs[1]) && fabsf(cs[0]) >= fabsf(cs[2]) ? 0u : (fabsf(cs[1]) >= fabsf(cs[2]) ? 1u : 2u);
+    if (cs[ax] < 0.0f) {
+        for (int k = 0; k < 6; ++k) {
+            const float t = f[k];
+            f[k] = f[6 + k];
+            f[6 + k] = t;
+        }
+        const int32_t t = ri;
+        ri = rj;
+        rj = t;
+    }
     nd.c0 = ri;
     nd.c1 = rj;
-    // split axis (for the render kernel's child order): the axis of the largest centroid separation
-    float cs[3];
-    for (int k = 0; k < 3; ++k) cs[k] = fabsf((f[6 + k] + f[9 + k]) - (f[k] + f[3 + k]));
-    nd.pad0 = cs[0] >= cs[1] && cs[0] >= cs[2] ? 0u : (cs[1] >= cs[2] ? 1u : 2u);
+    nd.pad0 = ax;
     nd.pad1 = 0;
     bin[id] = nd;
     if (ri < 0) leaf_parent[~ri] = (int32_t)id;
