@@ -42,14 +42,14 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 B");
 
-// 4-wide node collapsed from the binary LBVH (every even-depth binary node becomes one node whose
-// children are its children or grandchildren).  SoA inside the node so one lane-uniform pair of
-// s_load_dwordx16 brings all four boxes.  Empty slots hold a far point box that no ray can hit.
+// 4-wide node collapsed from the binary LBVH (every 4-wide node is a binary subtree opened greedily
+// by surface area).  Per child the box is stored as (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z): two scalar
+// loads bring the whole node, and each axis' (lo, hi) is an aligned SGPR pair, so one v_pk_fma_f32
+// gives both plane distances.  Empty slots hold a far point box that no ray can hit.
 constexpr int BVH_W = 4;
 constexpr float EMPTY_BOX = 3e37f;
 struct alignas(16) Bvh4Node {
-    float lox[4], loy[4], loz[4];
-    float hix[4], hiy[4], hiz[4];
+    float box[4][6];   // [child][lx, hx, ly, hy, lz, hz]
     int32_t child[4];  // >= 0: Bvh4Node index; < 0: leaf ~record index
     uint32_t nchild;
     uint32_t pad[3];   // [0] split axis of the children's order (0 x, 1 y, 2 z), [1] internal-child mask

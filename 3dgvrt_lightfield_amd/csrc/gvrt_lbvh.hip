@@ -232,8 +232,9 @@ __global__ __launch_bounds__(256) void k_even_flags(int64_t ni, const int32_t* _
 }
 
 __device__ inline void put_slot(Bvh4Node& o, int k, const float* b, int32_t ref) {
-    o.lox[k] = b[0]; o.loy[k] = b[1]; o.loz[k] = b[2];
-    o.hix[k] = b[3]; o.hiy[k] = b[4]; o.hiz[k] = b[5];
+    o.box[k][0] = b[0]; o.box[k][1] = b[3];  // x: lo, hi
+    o.box[k][2] = b[1]; o.box[k][3] = b[4];  // y
+    o.box[k][4] = b[2]; o.box[k][5] = b[5];  // z
     o.child[k] = ref;
 }
 
@@ -453,8 +454,10 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
         TRYH(hipStreamSynchronize(c->stream), "sync");
         for (int k = 0; k < 4; ++k) {
             const float* b = k == 0 ? hb : nullptr;
-            root.lox[k] = b ? b[0] : EMPTY_BOX; root.loy[k] = b ? b[1] : EMPTY_BOX; root.loz[k] = b ? b[2] : EMPTY_BOX;
-            root.hix[k] = b ? b[3] : EMPTY_BOX; root.hiy[k] = b ? b[4] : EMPTY_BOX; root.hiz[k] = b ? b[5] : EMPTY_BOX;
+            for (int a = 0; a < 3; ++a) {
+                root.box[k][2 * a] = b ? b[a] : EMPTY_BOX;
+                root.box[k][2 * a + 1] = b ? b[3 + a] : EMPTY_BOX;
+            }
             root.child[k] = k == 0 ? ~0 : 0;
         }
         root.nchild = 1;

@@ -48,6 +48,9 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 #ifndef GVRT_FMA_BOX
 #define GVRT_FMA_BOX 1
 #endif
+#ifndef GVRT_PK_BOX
+#define GVRT_PK_BOX 0  // packed-FMA box test: measured 3 % slower (more VGPRs for the broadcast pairs)
+#endif
 #ifndef GVRT_ORDER
 #define GVRT_ORDER 0
 #endif
@@ -78,6 +81,20 @@ __device__ inline bool box_hit(float lx, float ly, float lz, float hx, float hy,
 #endif
     const float tn = fmaxf(fmaxf(t0, fminf(ax, bx)), fmaxf(fminf(ay, by), fminf(az, bz)));
     const float tf = fminf(fminf(t1, fmaxf(ax, bx)), fminf(fmaxf(ay, by), fmaxf(az, bz)));
+    tenter = tn;
+    return tn <= tf + 2e-6f * fabsf(tf);
+}
+
+// Node box test on the (lo, hi) pair layout: one packed FMA per axis gives both plane distances
+// (v_pk_fma_f32 with the node's SGPR pair, the lane's 1/d and -o/d broadcast by op_sel), the same
+// values as box_hit's six FMAs.
+typedef float pf2 __attribute__((ext_vector_type(2)));
+__device__ inline bool box_hit_pk(const float* cb, f3 oinv, f3 inv, float t0, float t1, float& tenter) {
+    const pf2 X = __builtin_elementwise_fma(pf2{cb[0], cb[1]}, pf2{inv.x, inv.x}, pf2{-oinv.x, -oinv.x});
+    const pf2 Y = __builtin_elementwise_fma(pf2{cb[2], cb[3]}, pf2{inv.y, inv.y}, pf2{-oinv.y, -oinv.y});
+    const pf2 Z = __builtin_elementwise_fma(pf2{cb[4], cb[5]}, pf2{inv.z, inv.z}, pf2{-oinv.z, -oinv.z});
+    const float tn = fmaxf(fmaxf(t0, fminf(X.x, X.y)), fmaxf(fminf(Y.x, Y.y), fminf(Z.x, Z.y)));
+    const float tf = fminf(fminf(t1, fmaxf(X.x, X.y)), fminf(fmaxf(Y.x, Y.y), fmaxf(Z.x, Z.y)));
     tenter = tn;
     return tn <= tf + 2e-6f * fabsf(tf);
 }
@@ -447,18 +464,17 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
             const float tc = fminf(fminf(thi, kt[KB - 1]), tcut);
             float ent[4];
             uint64_t bal[4];
-#define GVRT_BOX4(TEST)                                                                                 \
-    _Pragma("unroll") for (int k = 0; k < 4; ++k) {                                                     \
-        const bool hit = TEST(nd.lox[k], nd.loy[k], nd.loz[k], nd.hix[k], nd.hiy[k], nd.hiz[k], oinv, inv, \
-                              tlo, tc, ent[k]);                                                         \
-        bal[k] = __builtin_amdgcn_ballot_w64(hit) & amask; /* compare result straight to an SGPR mask */ \
-    }
-#define GVRT_BOX_GENERIC(lx, ly, lz, hx, hy, hz, oi, iv, t0, t1, e) box_hit(lx, ly, lz, hx, hy, hz, o, oi, iv, t0, t1, e)
-            // (a per-octant min/max-free box test was measured slower: 9 code copies, or its plane
-            // swaps moved to SALU — the scalar unit is on the critical path)
-            GVRT_BOX4(GVRT_BOX_GENERIC)
-#undef GVRT_BOX_GENERIC
-#undef GVRT_BOX4
+            // (a per-octant min/max-free box test measured within noise: +0.7 %, 9 code copies)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float* cb = nd.box[k];
+#if GVRT_PK_BOX
+                const bool hit = box_hit_pk(cb, oinv, inv, tlo, tc, ent[k]);
+#else
+                const bool hit = box_hit(cb[0], cb[2], cb[4], cb[1], cb[3], cb[5], o, oinv, inv, tlo, tc, ent[k]);
+#endif
+                bal[k] = __builtin_amdgcn_ballot_w64(hit) & amask;  // compare result straight to an SGPR mask
+            }
             int32_t ch[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) ch[k] = unii(nd.child[k]);
