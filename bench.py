@@ -100,35 +100,59 @@ def main():
     mode = gv.MODE_FAST if args.mode == "fast" else gv.MODE_LITERAL
     params = r.render_params(mode=mode)
 
-    gathered = None
-    if distributed and rank == 0:
-        if args.split == "views":
-            gathered = [torch.empty_like(frame) for _ in range(world)]
-        else:
-            sizes = [gv.tiles_for_rank(W, H, 1, q, world, block=8).shape[0] * 64 for q in range(world)]
-            gathered = [torch.empty((s, 4), dtype=torch.uint8, device=dev) for s in sizes]
+    # Double-buffered frame exchange: the RCCL gather of frame i (torch's stream, async) runs while
+    # frame i+1 renders on the library's own HIP stream; a buffer is reused only after its gather
+    # completed.  Tile split: rank 0 scatters the gathered parts into the full frame
+    # (gvrt_unpack_tiles_rgba8), as SURVEY §8e's one exchange step per frame.
+    nbuf = 2 if distributed else 1
+    frames = [frame] + [torch.zeros_like(frame) for _ in range(nbuf - 1)]
+    rank_tiles = [gv.tiles_for_rank(W, H, 1, q, world, block=8) for q in range(world)] if args.split == "tiles" else None
     if distributed and args.split == "tiles":
         # NCCL gather needs equal sizes: pad every rank's part to the largest
-        maxs = max(gv.tiles_for_rank(W, H, 1, q, world, block=8).shape[0] for q in range(world)) * 64
-        sendbuf = torch.zeros((maxs, 4), dtype=torch.uint8, device=dev)
-        if rank == 0:
-            gathered = [torch.empty((maxs, 4), dtype=torch.uint8, device=dev) for _ in range(world)]
+        maxs = max(t.shape[0] for t in rank_tiles) * 64
+        sendbufs = [torch.zeros((maxs, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+        gathered = [[torch.empty((maxs, 4), dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
+                    for _ in range(nbuf)]
+        full = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
+    elif distributed:
+        gathered = [[torch.empty_like(frame) for _ in range(world)] if rank == 0 else None for _ in range(nbuf)]
+    pending = [None] * nbuf
 
     kernel_ms = []
 
+    def finish(b):
+        if pending[b] is None:
+            return
+        pending[b].wait()
+        torch.cuda.current_stream().synchronize()  # the library's stream reads / overwrites this buffer next
+        if args.split == "tiles" and rank == 0:
+            for q in range(world):
+                r.unpack_tiles_rgba8(gathered[b][q].data_ptr(), rank_tiles[q], W, H, full.data_ptr())
+        pending[b] = None
+
+    it = [0]
+
     def step():
-        r.render_device(vi, pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=frame.data_ptr(),
+        b = it[0] % nbuf
+        it[0] += 1
+        finish(b)
+        r.render_device(vi, pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=frames[b].data_ptr(),
                         packed=args.split == "tiles")
         kernel_ms.append(r.stats()["render_ms"])
         if distributed:
             if args.split == "views":
-                dist.gather(frame, gathered if rank == 0 else None, dst=0)
+                pending[b] = dist.gather(frames[b], gathered[b] if rank == 0 else None, dst=0, async_op=True)
             else:
-                sendbuf[: frame.shape[0]].copy_(frame)
-                dist.gather(sendbuf, gathered if rank == 0 else None, dst=0)
+                sendbufs[b][: frames[b].shape[0]].copy_(frames[b])
+                pending[b] = dist.gather(sendbufs[b], gathered[b] if rank == 0 else None, dst=0, async_op=True)
+
+    def drain():
+        for b in range(nbuf):
+            finish(b)
 
     for _ in range(args.warmup):
         step()
+    drain()
     kernel_ms.clear()
     if distributed:
         dist.barrier()
@@ -136,6 +160,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()  # every frame of the timed steps is rendered and gathered (and scattered) inside the clock
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
