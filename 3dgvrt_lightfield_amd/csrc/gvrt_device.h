@@ -46,15 +46,19 @@ static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 B");
 // by surface area).  Per child the box is stored as (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z): two scalar
 // loads bring the whole node, and each axis' (lo, hi) is an aligned SGPR pair, so one v_pk_fma_f32
 // gives both plane distances.  Empty slots hold a far point box that no ray can hit.
-constexpr int BVH_W = 4;
+#ifndef GVRT_BVH_W
+#define GVRT_BVH_W 4
+#endif
+constexpr int BVH_W = GVRT_BVH_W;  // children per node (4 or 8; build and render must agree)
+static_assert(BVH_W == 4 || BVH_W == 8, "4- or 8-wide nodes");
 constexpr float EMPTY_BOX = 3e37f;
-struct alignas(16) Bvh4Node {
-    float box[4][6];   // [child][lx, hx, ly, hy, lz, hz]
-    int32_t child[4];  // >= 0: Bvh4Node index; < 0: leaf ~record index
+struct alignas(16) Bvh4Node {  // (name kept from the 4-wide layout; BVH_W children)
+    float box[BVH_W][6];   // [child][lx, hx, ly, hy, lz, hz]
+    int32_t child[BVH_W];  // >= 0: node index; < 0: leaf ~record index
     uint32_t nchild;
-    uint32_t pad[3];   // [0] split axis of the children's order (0 x, 1 y, 2 z), [1] internal-child mask
+    uint32_t pad[3];       // [0] split axis of the children's order (0 x, 1 y, 2 z), [1] internal-child mask
 };
-static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node must be 128 B");
+static_assert(sizeof(Bvh4Node) == 28 * BVH_W + 16, "node layout: 128 B (4-wide) / 240 B (8-wide)");
 
 struct f3 {
     float x, y, z;

@@ -268,7 +268,7 @@ __global__ __launch_bounds__(256) void k_collapse(int64_t ni, const BvhNode* __r
     o.nchild = (uint32_t)k;
     uint32_t imask = 0;
     for (int j = 0; j < k; ++j) imask |= o.child[j] >= 0 ? (1u << j) : 0u;
-    for (; k < 4; ++k) put_slot(o, k, eb, 0);
+    for (; k < BVH_W; ++k) put_slot(o, k, eb, 0);
     o.pad[0] = n.pad0;
     o.pad[1] = imask;
     o.pad[2] = 0;
@@ -291,8 +291,8 @@ __global__ __launch_bounds__(256) void k_collapse_level(const BvhNode* __restric
     const uint64_t i = (uint64_t)begin + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= end) return;
     const BvhNode n = bin[src4[i]];
-    int32_t ref[4];
-    float box[4][6];
+    int32_t ref[BVH_W];
+    float box[BVH_W][6];
     const float* nb = reinterpret_cast<const float*>(&n);
     ref[0] = n.c0;
     ref[1] = n.c1;
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(256) void k_collapse_level(const BvhNode* __restric
         box[1][k] = nb[6 + k];
     }
     int cnt = 2;
-    while (cnt < 4) {
+    while (cnt < BVH_W) {
         int best = -1;
         float ba = -1.0f;
         for (int j = 0; j < cnt; ++j) {
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(256) void k_collapse_level(const BvhNode* __restric
     }
     const float eb[6] = {EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX};
     o.nchild = (uint32_t)cnt;
-    for (int j = cnt; j < 4; ++j) put_slot(o, j, eb, 0);
+    for (int j = cnt; j < BVH_W; ++j) put_slot(o, j, eb, 0);
     o.pad[0] = n.pad0;  // split axis of the binary root (children are in its in-order)
     o.pad[1] = imask;   // children that are 4-wide nodes
     o.pad[2] = 0;
@@ -452,7 +452,7 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
         float hb[6];
         TRYH(hipMemcpyAsync(hb, lboxes, 24, hipMemcpyDeviceToHost, c->stream), "leaf box");
         TRYH(hipStreamSynchronize(c->stream), "sync");
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < BVH_W; ++k) {
             const float* b = k == 0 ? hb : nullptr;
             for (int a = 0; a < 3; ++a) {
                 root.box[k][2 * a] = b ? b[a] : EMPTY_BOX;
@@ -487,7 +487,8 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
         TRYH(hipMemcpyAsync(&hd, dep, 4, hipMemcpyDeviceToHost, c->stream), "depth");
         const int64_t ni = m - 1;
         const char* ce = getenv("GVRT_COLLAPSE");
-        const bool greedy = ploc || !(ce && ce[0] == '0');  // the even-depth rule needs the Karras layout
+        // the even-depth rule needs the Karras layout and 4-wide nodes
+        const bool greedy = ploc || BVH_W != 4 || !(ce && ce[0] == '0');
         if (greedy) {
             // ---- greedy surface-area collapse, level by level (upper bound: one 4-wide node per binary node)
             int32_t* src4 = lpar;  // lpar (m entries) is free after k_depth
@@ -503,7 +504,7 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
                 hipLaunchKernelGGL(k_collapse_level, dim3((unsigned)((w + 255) / 256)), dim3(256), 0, c->stream, c->d_nodes,
                                    src4, ctl, lv, c->d_nodes4);
                 hipLaunchKernelGGL(k_level_advance, dim3(1), dim3(1), 0, c->stream, ctl);
-                width = width * 4 < (uint64_t)ni ? width * 4 : (uint64_t)ni;
+                width = width * BVH_W < (uint64_t)ni ? width * BVH_W : (uint64_t)ni;
             }
             TRYH(hipGetLastError(), "k_collapse_level");
             uint32_t hc[4];
@@ -545,8 +546,8 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
     cleanup();
 #undef TRY
 #undef TRYH
-    // the 4-wide traversal pushes at most 3 entries per 4-wide level
-    if (3 * c->depth4 + 2 > (uint32_t)STACK_DEPTH)
+    // the traversal pushes at most BVH_W - 1 entries per level
+    if ((BVH_W - 1) * c->depth4 + 2 > (uint32_t)STACK_DEPTH)
         return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "LBVH deeper than the render kernel's traversal stack");
     c->stats.bvh_nodes = c->n_nodes4;
     c->stats.bvh_depth = c->depth;

@@ -51,9 +51,6 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 #ifndef GVRT_PK_BOX
 #define GVRT_PK_BOX 0  // packed-FMA box test: measured 3 % slower (more VGPRs for the broadcast pairs)
 #endif
-#ifndef GVRT_ORDER
-#define GVRT_ORDER 0
-#endif
 #ifndef GVRT_TCUT
 #define GVRT_TCUT 1
 #endif
@@ -287,6 +284,16 @@ __device__ inline int32_t writelane(int32_t old, int32_t v, int32_t lane) {
     return old;
 }
 
+// arr[k] for a wave-uniform k: a select chain (s_cmp / s_cselect) over the register array.  A macro,
+// not a function taking the array by reference: that form pushed the arrays to scratch (+55 % time).
+#if GVRT_BVH_W == 4
+#define GVRT_PICK(a, k) ((k) == 0 ? (a)[0] : (k) == 1 ? (a)[1] : (k) == 2 ? (a)[2] : (a)[3])
+#else
+#define GVRT_PICK(a, k)                                                                                  \
+    ((k) == 0 ? (a)[0] : (k) == 1 ? (a)[1] : (k) == 2 ? (a)[2] : (k) == 3 ? (a)[3] : (k) == 4 ? (a)[4] \
+     : (k) == 5 ? (a)[5] : (k) == 6 ? (a)[6] : (a)[7])
+#endif
+
 __device__ inline uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ inline float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
@@ -458,15 +465,15 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
         float tcut = INF_DIST;  // termination-aware cull distance of this lane (see the leaf insert)
         const uint64_t amask = __builtin_amdgcn_ballot_w64(active);
         sp = 0;
-        Bvh4Node nd = nodes_[0];  // whole node: 2x s_load_dwordx16
+        Bvh4Node nd = nodes_[0];  // whole node: scalar loads (2x s_load_dwordx16 when 4-wide)
         while (true) {
             if constexpr (STATS) ++w_nodes;
             const float tc = fminf(fminf(thi, kt[KB - 1]), tcut);
-            float ent[4];
-            uint64_t bal[4];
+            float ent[BVH_W];
+            uint64_t bal[BVH_W];
             // (a per-octant min/max-free box test measured within noise: +0.7 %, 9 code copies)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < BVH_W; ++k) {
                 const float* cb = nd.box[k];
 #if GVRT_PK_BOX
                 const bool hit = box_hit_pk(cb, oinv, inv, tlo, tc, ent[k]);
@@ -475,21 +482,20 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
 #endif
                 bal[k] = __builtin_amdgcn_ballot_w64(hit) & amask;  // compare result straight to an SGPR mask
             }
-            int32_t ch[4];
+            int32_t ch[BVH_W];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) ch[k] = unii(nd.child[k]);
-#if GVRT_ORDER == 0
+            for (int k = 0; k < BVH_W; ++k) ch[k] = unii(nd.child[k]);
             // ---- children in the node's stored order (in-order of the binary split), forward when the
             // first lane's ray points along +axis, else backward: a handful of SALU ops per node
             // (the entry-distance sort below costs ~100)
             uint32_t hm = 0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) hm |= bal[k] ? (1u << k) : 0u;
+            for (int k = 0; k < BVH_W; ++k) hm |= bal[k] ? (1u << k) : 0u;
             const uint32_t inner = uni(nd.pad[1]);
             uint32_t leafmask = hm & ~inner;
             uint32_t im = hm & inner;
             int32_t next = -1;
-            auto chsel = [&](int k) { return k == 0 ? ch[0] : (k == 1 ? ch[1] : (k == 2 ? ch[2] : ch[3])); };
+            auto chsel = [&](int k) { return GVRT_PICK(ch, k); };
             if (im) {
                 const bool rev = (rsign >> uni(nd.pad[0])) & 1u;
                 const int first = rev ? 31 - __clz(im) : __ffs(im) - 1;
@@ -503,61 +509,16 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
             } else if (sp > 0) {
                 next = pop();
             }
-#else
-            uint32_t leafmask = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (bal[k] && ch[k] < 0) leafmask |= 1u << k;
-            }
-            leafmask = uni(leafmask);
-
-            // ---- choose the next node before the leaf work (uniform values: SALU).  Key = entry
-            // distance of the first lane that hits the child; distances are >= tlo > 0, so uint
-            // order = float order.  (A branch-free form of this block measured 8 % slower.)
-            uint32_t key[4];
-            int32_t cid[4];
-            int nint = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                key[k] = 0xFFFFFFFFu;
-                cid[k] = -1;
-                if (bal[k] && ch[k] >= 0) {
-                    key[k] = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(ent[k]), (int)__builtin_ctzll(bal[k]));
-                    cid[k] = ch[k];
-                    ++nint;
-                }
-            }
-            int32_t next = -1;
-            if (nint > 0) {
-                // sort the (key, child) pairs ascending: 5-comparator network
-#define GVRT_CX(i, j)                                          \
-    {                                                          \
-        const bool sw = key[j] < key[i];                       \
-        const uint32_t ki = key[i], kj = key[j];               \
-        const int32_t ci = cid[i], cj = cid[j];                \
-        key[i] = sw ? kj : ki;                                 \
-        key[j] = sw ? ki : kj;                                 \
-        cid[i] = sw ? cj : ci;                                 \
-        cid[j] = sw ? ci : cj;                                 \
-    }
-                GVRT_CX(0, 1) GVRT_CX(2, 3) GVRT_CX(0, 2) GVRT_CX(1, 3) GVRT_CX(1, 2)
-#undef GVRT_CX
-                // farther children on the stack, the second-nearest on top
-                for (int k = nint - 1; k >= 1; --k) push(cid[k]);
-                next = unii(cid[0]);
-            } else if (sp > 0) {
-                next = pop();
-            }
-
-#endif
+            // (sorting the hit children by the first hitting lane's entry distance instead cost ~100 SALU
+            // per node and visited more nodes: 2.79 vs 2.18 ms)
             // ---- leaves of this node (the k-buffer orders them); one rolled loop = one insertion
             // site; the next leaf's record load is issued before the current leaf's tests
 #pragma unroll 1
             while (leafmask) {
                 const int k = __builtin_ctz(leafmask);
                 leafmask &= leafmask - 1;
-                const uint64_t bk = k == 0 ? bal[0] : (k == 1 ? bal[1] : (k == 2 ? bal[2] : bal[3]));
-                const int32_t ck = k == 0 ? ch[0] : (k == 1 ? ch[1] : (k == 2 ? ch[2] : ch[3]));
+                const uint64_t bk = GVRT_PICK(bal, k);
+                const int32_t ck = GVRT_PICK(ch, k);
                 const RenderRec rec = recs_[~ck];
                 {
                     const uint32_t gi = uni((uint32_t)(~ck));
