@@ -10,9 +10,11 @@
 //   3. stable radix sort      (rocPRIM via hipcub, keys 63 bits, values = compaction index)
 //   4. permute records        (render records, SH, boxes into leaf order: leaf j = record j)
 //   5. Karras 2012 hierarchy  (one thread per internal node; index tie-break for equal codes)
-//   6. bottom-up AABB refit   (one thread per leaf; agent-scope acq_rel arrival counters)
+//   6. child boxes            (range-union sparse table over the leaf boxes, written by the hierarchy pass)
 //   7. depth census           (guards the render kernel's fixed LDS stack)
 #include <hipcub/hipcub.hpp>
+
+#include <vector>
 
 #include "gvrt_internal.h"
 
@@ -35,8 +37,8 @@ __host__ __device__ inline float ord2f(uint32_t u) {
 #endif
 }
 
-__global__ __launch_bounds__(256) void k_bounds(uint64_t m, const float* __restrict__ boxes,
-                                                uint32_t* __restrict__ out /*6: min xyz, max xyz (ordered)*/) {
+// centroid bounds, pass 1: one partial per block (block reduce in LDS, no contended atomics)
+__global__ __launch_bounds__(256) void k_bounds(uint64_t m, const float* __restrict__ boxes, float* __restrict__ part) {
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
 #pragma unroll
@@ -44,6 +46,42 @@ __global__ __launch_bounds__(256) void k_bounds(uint64_t m, const float* __restr
             const float c = 0.5f * (boxes[6 * i + k] + boxes[6 * i + 3 + k]);
             lo[k] = fminf(lo[k], c);
             hi[k] = fmaxf(hi[k], c);
+        }
+    }
+    __shared__ float red[4][6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        for (int off = 32; off > 0; off >>= 1) {
+            lo[k] = fminf(lo[k], __shfl_xor(lo[k], off));
+            hi[k] = fmaxf(hi[k], __shfl_xor(hi[k], off));
+        }
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            red[w][k] = lo[k];
+            red[w][3 + k] = hi[k];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int k = threadIdx.x;
+        float v = red[0][k];
+        for (int j = 1; j < 4; ++j) v = k < 3 ? fminf(v, red[j][k]) : fmaxf(v, red[j][k]);
+        part[6 * blockIdx.x + k] = v;
+    }
+}
+
+// pass 2: one block folds the partials into the ordered-uint bounds k_morton reads
+__global__ __launch_bounds__(256) void k_bounds_final(uint32_t nparts, const float* __restrict__ part,
+                                                      uint32_t* __restrict__ out) {
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = fminf(lo[k], part[6 * i + k]);
+            hi[k] = fmaxf(hi[k], part[6 * i + 3 + k]);
         }
     }
 #pragma unroll
@@ -110,6 +148,30 @@ __global__ __launch_bounds__(256) void k_permute(uint64_t m, const uint32_t* __r
     leaf_src[j] = s;
 }
 
+// Range-union sparse table over the leaf boxes (leaf order): level k holds, for every i, the union of
+// leaves [i, i + 2^k).  The box of any leaf range [l, r] is then the union of two level-k entries
+// (k = floor(log2(r - l + 1))) — min / max are exact and order-free, so the result is bit-identical
+// to a bottom-up refit, without the refit's per-level cross-XCD atomics.
+__global__ __launch_bounds__(256) void k_sparse_level(uint64_t m, uint64_t half, const float* __restrict__ prev,
+                                                      float* __restrict__ cur) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i + 2 * half > m) return;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const float a = prev[6 * i + k], b = prev[6 * (i + half) + k];
+        cur[6 * i + k] = k < 3 ? fminf(a, b) : fmaxf(a, b);
+    }
+}
+
+__device__ inline void range_box(const float* const* __restrict__ lv, int64_t l, int64_t r, float* out) {
+    const uint64_t len = (uint64_t)(r - l + 1);
+    const int k = 63 - __clzll(len);
+    const float* a = lv[k] + 6 * l;
+    const float* b = lv[k] + 6 * (r - ((int64_t)1 << k) + 1);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) out[j] = j < 3 ? fminf(a[j], b[j]) : fmaxf(a[j], b[j]);
+}
+
 __device__ inline int delta(const uint64_t* __restrict__ codes, int64_t m, int64_t i, int64_t j) {
     if (j < 0 || j >= m) return -1;
     const uint64_t a = codes[i], b = codes[j];
@@ -119,7 +181,8 @@ __device__ inline int delta(const uint64_t* __restrict__ codes, int64_t m, int64
 
 // Karras, "Maximizing Parallelism in the Construction of BVHs, Octrees, and k-d Trees", HPG 2012.
 __global__ __launch_bounds__(256) void k_karras(int64_t m, const uint64_t* __restrict__ codes, BvhNode* __restrict__ nodes,
-                                                int32_t* __restrict__ leaf_parent, int32_t* __restrict__ node_parent) {
+                                                int32_t* __restrict__ leaf_parent, int32_t* __restrict__ node_parent,
+                                                const float* const* __restrict__ levels) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m - 1) return;
     const int d = (delta(codes, m, i, i + 1) - delta(codes, m, i, i - 1)) >= 0 ? 1 : -1;
@@ -156,48 +219,22 @@ __global__ __launch_bounds__(256) void k_karras(int64_t m, const uint64_t* __res
     }
     nodes[i].c0 = c0;
     nodes[i].c1 = c1;
+    // child boxes straight from the leaf ranges [lo, gamma] and [gamma + 1, hi]
+    float b0[6], b1[6];
+    range_box(levels, lo, gamma, b0);
+    range_box(levels, gamma + 1, hi, b1);
+    float* nf = reinterpret_cast<float*>(nodes + i);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        nf[k] = b0[k];
+        nf[6 + k] = b1[k];
+    }
     // split axis: the first Morton bit where the range differs (bit 3b+2 = x, 3b+1 = y, 3b = z); c0 is the
     // lower side, so the render kernel can order children by the ray's direction on this axis
     const int p = 63 - dnode;
     nodes[i].pad0 = dnode >= 64 ? 0u : (uint32_t)(2 - p % 3);
     nodes[i].pad1 = 0;
     if (i == 0) node_parent[0] = -1;
-}
-
-__device__ inline void store_slot(BvhNode* nd, int slot, const float b[6]) {
-    float* f = reinterpret_cast<float*>(nd) + 6 * slot;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) f[k] = b[k];
-}
-
-__global__ __launch_bounds__(256) void k_refit(int64_t m, const float* __restrict__ leaf_boxes, BvhNode* nodes,
-                                               const int32_t* __restrict__ leaf_parent, const int32_t* __restrict__ node_parent,
-                                               uint32_t* counters) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= m) return;
-    float b[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) b[k] = leaf_boxes[6 * j + k];
-    int32_t child = ~(int32_t)j;
-    int32_t p = leaf_parent[j];
-    while (p >= 0) {
-        BvhNode* nd = nodes + p;
-        const int slot = (nd->c0 == child) ? 0 : 1;
-        store_slot(nd, slot, b);
-        // release our slot, acquire the sibling's: agent scope (per-XCD L2s are not coherent)
-        const uint32_t old = __hip_atomic_fetch_add(counters + p, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == 0) return;  // first arrival: the sibling's thread continues
-        const float* f = reinterpret_cast<const float*>(nd);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            b[k] = fminf(__hip_atomic_load(f + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __hip_atomic_load(f + 6 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            b[3 + k] = fmaxf(__hip_atomic_load(f + 3 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                             __hip_atomic_load(f + 9 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        }
-        child = p;
-        p = node_parent[p];
-    }
 }
 
 __global__ __launch_bounds__(256) void k_depth(int64_t m, const int32_t* __restrict__ leaf_parent,
@@ -385,7 +422,9 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
     if ((s = gvrt_dalloc(c, (void**)&c->d_leaf_src, 4ull * m))) return s;
 
     // scratch
-    uint32_t *bnd = nullptr, *vals = nullptr, *vals2 = nullptr, *counters = nullptr, *dep = nullptr;
+    uint32_t *bnd = nullptr, *vals = nullptr, *vals2 = nullptr, *dep = nullptr;
+    float *stab = nullptr, *bpart = nullptr;
+    float** dlv = nullptr;
     uint64_t *keys = nullptr, *keys2 = nullptr;
     int32_t *lpar = nullptr, *npar = nullptr;
     float* lboxes = nullptr;
@@ -396,7 +435,9 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
         gvrt_dfree(c, (void**)&vals);
         gvrt_dfree(c, (void**)&keys2);
         gvrt_dfree(c, (void**)&vals2);
-        gvrt_dfree(c, (void**)&counters);
+        gvrt_dfree(c, (void**)&stab);
+        gvrt_dfree(c, (void**)&dlv);
+        gvrt_dfree(c, (void**)&bpart);
         gvrt_dfree(c, (void**)&dep);
         gvrt_dfree(c, (void**)&lpar);
         gvrt_dfree(c, (void**)&npar);
@@ -423,18 +464,26 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
     TRY(gvrt_dalloc(c, (void**)&vals, 4ull * m));
     TRY(gvrt_dalloc(c, (void**)&keys2, 8ull * m));
     TRY(gvrt_dalloc(c, (void**)&vals2, 4ull * m));
-    TRY(gvrt_dalloc(c, (void**)&counters, 4ull * ninternal));
+    // sparse-table levels 1 .. L-1 (level 0 = the leaf boxes themselves)
+    int nlev = 1;
+    while (((uint64_t)1 << nlev) <= (uint64_t)m) ++nlev;
+    std::vector<const float*> hlv(nlev, nullptr);
+    if (nlev > 1) TRY(gvrt_dalloc(c, (void**)&stab, 24ull * m * (nlev - 1)));
+    TRY(gvrt_dalloc(c, (void**)&dlv, sizeof(float*) * nlev));
     TRY(gvrt_dalloc(c, (void**)&dep, 32));
     TRY(gvrt_dalloc(c, (void**)&lpar, 4ull * m));
     TRY(gvrt_dalloc(c, (void**)&npar, 4ull * ninternal));
     TRY(gvrt_dalloc(c, (void**)&lboxes, 24ull * m));
 
+    const unsigned blocks = (unsigned)((m + 255) / 256);
+    const unsigned rblocks = blocks < 1024 ? blocks : 1024;
+    TRY(gvrt_dalloc(c, (void**)&bpart, 24ull * rblocks));
+
     TRYH(hipEventRecord(c->ev0, c->stream), "event");
     const uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
     TRYH(hipMemcpyAsync(bnd, init, 24, hipMemcpyHostToDevice, c->stream), "bounds init");
-    const unsigned blocks = (unsigned)((m + 255) / 256);
-    const unsigned rblocks = blocks < 2048 ? blocks : 2048;
-    hipLaunchKernelGGL(k_bounds, dim3(rblocks), dim3(256), 0, c->stream, (uint64_t)m, c->d_boxes_c, bnd);
+    hipLaunchKernelGGL(k_bounds, dim3(rblocks), dim3(256), 0, c->stream, (uint64_t)m, c->d_boxes_c, bpart);
+    hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(256), 0, c->stream, rblocks, bpart, bnd);
     hipLaunchKernelGGL(k_morton, dim3(blocks), dim3(256), 0, c->stream, (uint64_t)m, c->d_boxes_c, bnd, keys, vals);
     TRYH(hipGetLastError(), "k_morton");
     size_t tmp_bytes = 0;
@@ -468,7 +517,6 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
         c->depth = 1;
         c->depth4 = 1;
     } else {
-        TRYH(hipMemsetAsync(counters, 0, 4ull * ninternal, c->stream), "memset");
         TRYH(hipMemsetAsync(dep, 0, 4, c->stream), "memset");
         const char* be = getenv("GVRT_BUILDER");
         const bool ploc = be && be[0] == 'p';  // "ploc": measured 3 % slower to render (more visits), see DESIGN.md
@@ -477,12 +525,22 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
             uint32_t iters = 0;
             TRY(gvrt_ploc_build(c, (uint32_t)m, lboxes, c->d_nodes, lpar, npar, &root, &iters));
         } else {
+            // leaf-range union table, then the hierarchy with its child boxes in one pass (no refit)
+            hlv[0] = lboxes;
+            for (int k = 1; k < nlev; ++k) {
+                hlv[k] = stab + 6ull * m * (k - 1);
+                const uint64_t half = (uint64_t)1 << (k - 1);
+                const uint64_t cnt = (uint64_t)m - 2 * half + 1;
+                hipLaunchKernelGGL(k_sparse_level, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, c->stream,
+                                   (uint64_t)m, half, hlv[k - 1], const_cast<float*>(hlv[k]));
+            }
+            TRYH(hipMemcpyAsync(dlv, hlv.data(), sizeof(float*) * nlev, hipMemcpyHostToDevice, c->stream), "levels");
             const unsigned iblocks = (unsigned)((m - 1 + 255) / 256);
-            hipLaunchKernelGGL(k_karras, dim3(iblocks), dim3(256), 0, c->stream, m, keys2, c->d_nodes, lpar, npar);
-            hipLaunchKernelGGL(k_refit, dim3(blocks), dim3(256), 0, c->stream, m, lboxes, c->d_nodes, lpar, npar, counters);
+            hipLaunchKernelGGL(k_karras, dim3(iblocks), dim3(256), 0, c->stream, m, keys2, c->d_nodes, lpar, npar,
+                               (const float* const*)dlv);
         }
         hipLaunchKernelGGL(k_depth, dim3(blocks), dim3(256), 0, c->stream, m, lpar, npar, dep);
-        TRYH(hipGetLastError(), "k_karras/k_refit");
+        TRYH(hipGetLastError(), "k_karras");
         uint32_t hd = 0;
         TRYH(hipMemcpyAsync(&hd, dep, 4, hipMemcpyDeviceToHost, c->stream), "depth");
         const int64_t ni = m - 1;
