@@ -51,6 +51,9 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 #ifndef GVRT_PK_BOX
 #define GVRT_PK_BOX 0  // packed-FMA box test: measured 3 % slower (more VGPRs for the broadcast pairs)
 #endif
+#ifndef GVRT_SH_PREFETCH
+#define GVRT_SH_PREFETCH 1
+#endif
 #ifndef GVRT_TCUT
 #define GVRT_TCUT 1
 #endif
@@ -612,27 +615,42 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                         uint32_t hid;
                         float halpha;
                         bool hacc;
+                        hid = PACK ? (kid[0] >> 8) : kid[0];
+#if GVRT_SH_PREFETCH
+                        // the SH address needs only the id: issue all 12 loads with the record's, one
+                        // memory round trip per hit instead of one per dependent chunk
+                        float4 shv[12];
+                        {
+                            const float4* s4 = reinterpret_cast<const float4*>(sh_ + 48ull * hid);
+#pragma unroll
+                            for (int j = 0; j < 12; ++j) shv[j] = s4[j];
+                        }
+#endif
                         if constexpr (PACK) {
                             // processHit re-evaluates the response of the hit particle (per-lane record load)
-                            hid = kid[0] >> 8;
                             const RenderRec rec = recs_[hid];
                             f3 ok, dk;
                             kernel_frame(rec, o, d, ok, dk);
                             const float l2 = len2(dk);
                             hacc = particle_alpha(ok, dk, l2, rec.density, a.min_response, a.alpha_min, halpha);
                         } else {
-                            hid = kid[0];
                             halpha = ka[0];
                             hacc = ka[0] > 0.0f;
                         }
                         if (hacc) {
                             const float weight = halpha * T;
-                            const float4* s4 = reinterpret_cast<const float4*>(sh_ + 48ull * hid);
                             float rr = 0.f, rg = 0.f, rb = 0.f;
+#if GVRT_SH_PREFETCH
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const float4 v0 = shv[3 * q], v1 = shv[3 * q + 1], v2 = shv[3 * q + 2];
+#else
+                            const float4* s4 = reinterpret_cast<const float4*>(sh_ + 48ull * hid);
                             // 16 coefficients x rgb = 12 float4, in 4 rolled chunks of 3 (few live VGPRs)
 #pragma unroll 1
                             for (int q = 0; q < 4; ++q) {
                                 const float4 v0 = s4[3 * q], v1 = s4[3 * q + 1], v2 = s4[3 * q + 2];
+#endif
                                 const float4 bq = s_basis[wid][q][lane];
                                 const float b0 = bq.x, b1 = bq.y, b2 = bq.z, b3 = bq.w;
                                 // coefficients 4q..4q+3: (v0.xyz) (v0.w v1.xy) (v1.zw v2.x) (v2.yzw)
