@@ -65,7 +65,8 @@ class Stats(C.Structure):
                 ("crossings", C.c_uint64), ("accepted", C.c_uint64), ("rounds", C.c_uint64),
                 ("enclose_ms", C.c_float), ("accel_ms", C.c_float), ("render_ms", C.c_float),
                 ("pad1", C.c_float), ("device_bytes", C.c_uint64), ("wave_node_visits", C.c_uint64),
-                ("wave_leaf_visits", C.c_uint64), ("lane_leaf_tests", C.c_uint64)]
+                ("wave_leaf_visits", C.c_uint64), ("lane_leaf_tests", C.c_uint64),
+                ("phase_cycles", C.c_uint64 * 4), ("wave_dead_visits", C.c_uint64)]
 
 
 H = C.c_void_p

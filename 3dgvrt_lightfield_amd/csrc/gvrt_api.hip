@@ -121,7 +121,7 @@ gvrt_status gvrt_create(int device, gvrt_handle* out) {
         delete c;
         return s;
     }
-    if (gvrt_dalloc(c, (void**)&c->d_stats, 64) != GVRT_OK) {
+    if (gvrt_dalloc(c, (void**)&c->d_stats, 128) != GVRT_OK) {
         delete c;
         return gvrt_fail(nullptr, GVRT_ERR_OOM, "stats alloc");
     }
@@ -356,7 +356,7 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
         }
     }
     if (c->stats_on) {
-        GVRT_HIP(c, hipMemsetAsync(c->d_stats, 0, 48, c->stream));
+        GVRT_HIP(c, hipMemsetAsync(c->d_stats, 0, 88, c->stream));
         a.stats = c->d_stats;
     }
     GVRT_HIP(c, hipEventRecord(c->ev0, c->stream));
@@ -368,8 +368,8 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
         if (bhc) GVRT_HIP(c, hipMemcpyAsync(out->hit_counts, a.hit_counts, bhc, hipMemcpyDeviceToHost, c->stream));
         if (b8) GVRT_HIP(c, hipMemcpyAsync(out->rgba8, a.rgba8, b8, hipMemcpyDeviceToHost, c->stream));
     }
-    unsigned long long hs[6] = {0, 0, 0, 0, 0, 0};
-    if (c->stats_on) GVRT_HIP(c, hipMemcpyAsync(hs, c->d_stats, 48, hipMemcpyDeviceToHost, c->stream));
+    unsigned long long hs[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (c->stats_on) GVRT_HIP(c, hipMemcpyAsync(hs, c->d_stats, 88, hipMemcpyDeviceToHost, c->stream));
     GVRT_HIP(c, hipStreamSynchronize(c->stream));
     float ms = 0.f;
     GVRT_HIP(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
@@ -381,6 +381,8 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
     c->stats.wave_node_visits = hs[3];
     c->stats.wave_leaf_visits = hs[4];
     c->stats.lane_leaf_tests = hs[5];
+    for (int k = 0; k < 4; ++k) c->stats.phase_cycles[k] = hs[6 + k];
+    c->stats.wave_dead_visits = hs[10];
     return GVRT_OK;
 }
 

@@ -390,6 +390,10 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
     // recovered exactly from the alpha accumulator (RQ/RT alpha = alpha_init + #accepted, Q10)
     uint32_t nproc = 0, rounds = 0;
     uint32_t w_nodes = 0, w_leaves = 0, l_leaves = 0;  // wave node visits, wave leaf visits, lane leaf tests
+    // STATS phase timers (s_memtime, wave-uniform): node visits, leaves + insertion, composite
+    uint64_t cyc_node = 0, cyc_leaf = 0, cyc_comp = 0;
+    uint32_t w_dead = 0;  // node visits where no lane hits any child box
+    [[maybe_unused]] const uint64_t cyc_start = STATS ? __builtin_amdgcn_s_memtime() : 0;
     bool active = valid && a.nrecs > 0 && (fmaxf(0.0f, tminb - EPS_T) <= tmaxb) && (1.0f > a.min_transmittance);
 
     static_assert(!(LITERAL && PACK), "LITERAL keeps rejected crossings: unpacked k-buffer");
@@ -470,7 +474,11 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
         sp = 0;
         Bvh4Node nd = nodes_[0];  // whole node: scalar loads (2x s_load_dwordx16 when 4-wide)
         while (true) {
-            if constexpr (STATS) ++w_nodes;
+            [[maybe_unused]] uint64_t t_node0 = 0;
+            if constexpr (STATS) {
+                ++w_nodes;
+                t_node0 = __builtin_amdgcn_s_memtime();
+            }
             const float tc = fminf(fminf(thi, kt[KB - 1]), tcut);
             float ent[BVH_W];
             uint64_t bal[BVH_W];
@@ -494,6 +502,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
             uint32_t hm = 0;
 #pragma unroll
             for (int k = 0; k < BVH_W; ++k) hm |= bal[k] ? (1u << k) : 0u;
+            if constexpr (STATS) w_dead += hm == 0 ? 1u : 0u;
             const uint32_t inner = uni(nd.pad[1]);
             uint32_t leafmask = hm & ~inner;
             uint32_t im = hm & inner;
@@ -514,6 +523,11 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
             }
             // (sorting the hit children by the first hitting lane's entry distance instead cost ~100 SALU
             // per node and visited more nodes: 2.79 vs 2.18 ms)
+            [[maybe_unused]] uint64_t t_leaf0 = 0;
+            if constexpr (STATS) {
+                t_leaf0 = __builtin_amdgcn_s_memtime();
+                cyc_node += t_leaf0 - t_node0;
+            }
             // ---- leaves of this node (the k-buffer orders them); one rolled loop = one insertion
             // site; the next leaf's record load is issued before the current leaf's tests
 #pragma unroll 1
@@ -593,11 +607,13 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                     }
                 }
             }
+            if constexpr (STATS) cyc_leaf += __builtin_amdgcn_s_memtime() - t_leaf0;
             if (next < 0) break;
             nd = nodes_[unii(next)];  // uniform by construction; readfirstlane lets the compiler see it
         }
 
         // ---------------- process k hits (particleRendering.comp:153-187)
+        [[maybe_unused]] const uint64_t t_comp0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
         if (active) {
             if (kid[0] == INVALID_ID) {
                 active = false;
@@ -684,6 +700,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                 s_acc[wid][lane] = acc;
             }
         }
+        if constexpr (STATS) cyc_comp += __builtin_amdgcn_s_memtime() - t_comp0;
     }
 
     // ---------------- outputs
@@ -725,6 +742,11 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
             atomicAdd(stats_ + 3, (unsigned long long)w_nodes);
             atomicAdd(stats_ + 4, (unsigned long long)w_leaves);
             atomicAdd(stats_ + 5, s5);
+            atomicAdd(stats_ + 6, (unsigned long long)cyc_node);
+            atomicAdd(stats_ + 7, (unsigned long long)cyc_leaf);
+            atomicAdd(stats_ + 8, (unsigned long long)cyc_comp);
+            atomicAdd(stats_ + 9, (unsigned long long)(__builtin_amdgcn_s_memtime() - cyc_start));
+            atomicAdd(stats_ + 10, (unsigned long long)w_dead);
         }
     }
 }

@@ -138,7 +138,9 @@ class Renderer:
     def stats(self):
         s = _lib.Stats()
         check(lib().gvrt_get_stats(self.h, C.byref(s)), self.h)
-        return {k: getattr(s, k) for k, _ in s._fields_ if not k.startswith("pad")}
+        out = {k: getattr(s, k) for k, _ in s._fields_ if not k.startswith("pad")}
+        out["phase_cycles"] = list(out["phase_cycles"])
+        return out
 
     @staticmethod
     def tile_array(tiles):

@@ -113,6 +113,9 @@ typedef struct {
     uint64_t wave_node_visits;  /* traversal diagnostics of the last render (stats enabled): */
     uint64_t wave_leaf_visits;  /*   BVH nodes / leaves visited per wave, summed over waves,  */
     uint64_t lane_leaf_tests;   /*   and ray-proxy clip tests summed over lanes               */
+    uint64_t phase_cycles[4];   /* s_memtime cycles summed over waves (stats enabled): node visits,
+                                   leaf tests + k-buffer insertion, compositing, whole kernel */
+    uint64_t wave_dead_visits;  /* node visits in which no lane hit any child box */
 } gvrt_stats;
 
 /* --------------------------------------------------------------------------------------- */

@@ -37,5 +37,11 @@ with gv.Renderer(0) as r:
                      "accepted/ray": round(st["accepted"] / rays, 3), "rounds/ray": round(st["rounds"] / rays, 3),
                      "node_visits/wave": round(st["wave_node_visits"] / waves, 1),
                      "leaf_visits/wave": round(st["wave_leaf_visits"] / waves, 1),
+                     "dead_visits/wave": round(st["wave_dead_visits"] / waves, 1),
                      "lane_leaf_tests/ray": round(st["lane_leaf_tests"] / rays, 2), "bvh_depth": st["bvh_depth"], "bvh_nodes": st["bvh_nodes"], "accel_ms": round(st["accel_ms"], 2)}
+        pc = st["phase_cycles"]
+        if pc[3]:
+            out[name]["phase_frac"] = {"node": round(pc[0] / pc[3], 3), "leaf+insert": round(pc[1] / pc[3], 3),
+                                       "composite": round(pc[2] / pc[3], 3),
+                                       "cycles/wave": round(pc[3] / waves)}
 print(json.dumps(out, indent=1))
