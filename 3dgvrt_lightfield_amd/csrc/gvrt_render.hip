@@ -781,7 +781,9 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
         else hipLaunchKernelGGL((k_render<L, A, K, false, P>), g, b, 0, c->stream, a, KARGS);         \
     } while (0)
     // packed payload needs record ids below 2^24 - 1 (id << 8 | q, all-ones = empty slot)
-    const bool pack = a.nrecs < 0xFFFFFFu;
+    // (GVRT_NO_PACK forces the unpacked path, which scenes of >= 2^24 - 1 survivors take, for testing)
+    static const bool no_pack = getenv("GVRT_NO_PACK") != nullptr;
+    const bool pack = a.nrecs < 0xFFFFFFu && !no_pack;
     if (literal) {  // the reference's 16-slot k-buffer (MAX_HIT_PER_TRACE)
         if (adaptive) GVRT_LAUNCH(true, true, K_HITS, false);
         else GVRT_LAUNCH(true, false, K_HITS, false);
