@@ -59,6 +59,10 @@ class Image(C.Structure):
                 ("hit_counts", C.c_void_p), ("device_ptrs", C.c_uint32), ("packed", C.c_uint32)]
 
 
+class AccelParams(C.Structure):
+    _fields_ = [("split_cells", C.c_uint32), ("builder", C.c_uint32), ("reserved", C.c_uint32 * 6)]
+
+
 class Stats(C.Structure):
     _fields_ = [("n_input", C.c_uint64), ("n_survivors", C.c_uint64), ("bvh_nodes", C.c_uint64),
                 ("bvh_depth", C.c_uint32), ("pad0", C.c_uint32), ("rays", C.c_uint64),
@@ -66,7 +70,8 @@ class Stats(C.Structure):
                 ("enclose_ms", C.c_float), ("accel_ms", C.c_float), ("render_ms", C.c_float),
                 ("pad1", C.c_float), ("device_bytes", C.c_uint64), ("wave_node_visits", C.c_uint64),
                 ("wave_leaf_visits", C.c_uint64), ("lane_leaf_tests", C.c_uint64),
-                ("phase_cycles", C.c_uint64 * 4), ("wave_dead_visits", C.c_uint64)]
+                ("phase_cycles", C.c_uint64 * 4), ("wave_dead_visits", C.c_uint64),
+                ("bvh_leaves", C.c_uint64)]
 
 
 H = C.c_void_p
@@ -86,6 +91,8 @@ SIGNATURES = {
     "gvrt_build_enclosing": (C.c_int32, [H, _P(EnclosingParams), _P(C.c_uint64)]),
     "gvrt_read_enclosing": (C.c_int32, [H, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "gvrt_build_accel": (C.c_int32, [H]),
+    "gvrt_build_accel_ex": (C.c_int32, [H, _P(AccelParams)]),
+    "gvrt_default_accel_params": (None, [_P(AccelParams)]),
     "gvrt_render": (C.c_int32, [H, _P(RenderParams), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
                                 C.c_uint32, C.c_void_p, C.c_uint64, _P(Image)]),
     "gvrt_set_stats": (C.c_int32, [H, C.c_int]),

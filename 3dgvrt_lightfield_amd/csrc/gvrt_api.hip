@@ -222,12 +222,24 @@ gvrt_status gvrt_read_enclosing(gvrt_handle c, float* density12, float* sh48, fl
     return GVRT_OK;
 }
 
-gvrt_status gvrt_build_accel(gvrt_handle c) {
+void gvrt_default_accel_params(gvrt_accel_params* p) {
+    if (!p) return;
+    *p = gvrt_accel_params{};
+}
+
+gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
     if (!c) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL handle");
     if (!c->enclosed) return gvrt_fail(c, GVRT_ERR_STATE, "gvrt_build_enclosing has not been called");
+    gvrt_accel_params d;
+    gvrt_default_accel_params(&d);
+    if (!p) p = &d;
+    if (p->split_cells > 1023) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "split_cells must be <= 1023");
+    if (p->builder > 1) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "builder must be 0 (LBVH) or 1 (PLOC)");
     GVRT_HIP(c, hipSetDevice(c->device));
-    return gvrt_launch_build_accel(c);
+    return gvrt_launch_build_accel(c, *p);
 }
+
+gvrt_status gvrt_build_accel(gvrt_handle c) { return gvrt_build_accel_ex(c, nullptr); }
 
 gvrt_status gvrt_set_stats(gvrt_handle c, int enable) {
     if (!c) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL handle");
@@ -279,7 +291,12 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
     RenderArgs a;
     std::memset(&a, 0, sizeof(a));
     a.recs = c->d_recs;
-    a.sh = c->d_sh;
+    // split: the k-buffer holds proxy (compaction) ids, shared by the proxy's pieces
+    a.crecs = c->split_cells ? c->d_recs_c : c->d_recs;
+    a.sh = c->split_cells ? c->d_sh48 : c->d_sh;
+    a.aux = reinterpret_cast<const uint4*>(c->d_leaf_aux);
+    for (int k = 0; k < 3; ++k) a.grid_min[k] = c->grid_min[k];
+    a.grid_inv = c->grid_inv;
     a.nodes = c->d_nodes4;
     a.nrecs = (uint32_t)c->m;
     // cameras

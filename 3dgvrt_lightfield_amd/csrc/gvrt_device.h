@@ -75,8 +75,10 @@ __host__ __device__ inline f3 cross3(f3 a, f3 b) {
 
 // Render-kernel launch arguments (one struct, passed by value).
 struct RenderArgs {
-    const RenderRec* __restrict__ recs;
-    const float* __restrict__ sh;        // 48 f32 per record
+    const RenderRec* __restrict__ recs;  // leaf order (one per BVH leaf)
+    const RenderRec* __restrict__ crecs; // by k-buffer id: = recs, or the compaction order when split
+    const float* __restrict__ sh;        // 48 f32 per k-buffer id
+    const uint4* __restrict__ aux;       // split: per leaf {proxy, cell, cell range lo, hi}; else null
     const Bvh4Node* __restrict__ nodes;
     const float* __restrict__ view_inv;  // 16 per camera, column-major
     const uint32_t* __restrict__ tiles;  // packed (cam<<24 | ty<<12 | tx) or null
@@ -102,6 +104,8 @@ struct RenderArgs {
     uint32_t ray_dirs_layout;
     uint32_t packed;
     uint32_t kfast;  // FAST-mode k-buffer depth (8, 12, 16, 24)
+    float grid_min[3];  // split grid (SplitBLAS analogue): origin and 1 / cell size
+    float grid_inv;
     uint8_t* rgba8;
     float* rgba32f;
     float* ray_dirs;

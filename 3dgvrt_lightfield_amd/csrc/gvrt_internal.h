@@ -48,6 +48,12 @@ struct gvrt_context {
     gvrt::Bvh4Node* d_nodes4 = nullptr; // 4-wide collapse traversed by the render kernel
     uint64_t n_nodes4 = 0;
     uint32_t* d_leaf_src = nullptr;  // leaf -> compaction index
+    uint64_t n_leaves = 0;           // BVH leaves: the survivors, or their split pieces
+    uint32_t* d_leaf_aux = nullptr;  // split: per leaf {proxy, cell, proxy's cell range lo, hi} (uint4); else null
+    uint32_t split_cells = 0;        // grid cells on the longest axis (0: no split)
+    float grid_min[3] = {0, 0, 0};
+    float grid_inv = 0.0f;           // 1 / cell size
+    uint32_t grid_n[3] = {0, 0, 0};
     uint32_t depth = 0;   // binary LBVH depth
     uint32_t depth4 = 0;  // 4-wide levels (bounds the traversal stack: 3 pushes per level)
 
@@ -78,7 +84,7 @@ void gvrt_dfree(gvrt_context* c, void** p);
 // gvrt_enclose.hip
 gvrt_status gvrt_launch_enclose(gvrt_context* c, const gvrt_enclosing_params* p, uint64_t* m);
 // gvrt_lbvh.hip
-gvrt_status gvrt_launch_build_accel(gvrt_context* c);
+gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& p);
 gvrt_status gvrt_ploc_build(gvrt_context* c, uint32_t m, const float* leaf_boxes, gvrt::BvhNode* bin,
                             int32_t* leaf_parent, int32_t* node_parent, int32_t* root, uint32_t* iterations);
 // gvrt_render.hip

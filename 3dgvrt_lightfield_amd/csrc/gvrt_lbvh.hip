@@ -37,15 +37,18 @@ __host__ __device__ inline float ord2f(uint32_t u) {
 #endif
 }
 
-// centroid bounds, pass 1: one partial per block (block reduce in LDS, no contended atomics)
+// bounds of the box centroids (CENTROID) or of the boxes themselves, pass 1: one partial per block
+// (block reduce in LDS, no contended atomics)
+template <bool CENTROID>
 __global__ __launch_bounds__(256) void k_bounds(uint64_t m, const float* __restrict__ boxes, float* __restrict__ part) {
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const float c = 0.5f * (boxes[6 * i + k] + boxes[6 * i + 3 + k]);
-            lo[k] = fminf(lo[k], c);
-            hi[k] = fmaxf(hi[k], c);
+            const float bl = boxes[6 * i + k], bh = boxes[6 * i + 3 + k];
+            const float c = 0.5f * (bl + bh);
+            lo[k] = fminf(lo[k], CENTROID ? c : bl);
+            hi[k] = fmaxf(hi[k], CENTROID ? c : bh);
         }
     }
     __shared__ float red[4][6];
@@ -131,21 +134,100 @@ __global__ __launch_bounds__(256) void k_morton(uint64_t m, const float* __restr
     vals[i] = (uint32_t)i;
 }
 
+// Leaf order: leaf j takes sorted item perm[j] (a proxy, or a split piece whose proxy is psrc[.]).
+// Records are copied per leaf; the SH only without split (with split the k-buffer payload is the
+// proxy id and the SH / composite records stay in compaction order).
 __global__ __launch_bounds__(256) void k_permute(uint64_t m, const uint32_t* __restrict__ perm, const RenderRec* __restrict__ rin,
                                                  const float* __restrict__ shin, const float* __restrict__ bin,
-                                                 RenderRec* __restrict__ rout, float* __restrict__ shout,
-                                                 float* __restrict__ bout, uint32_t* __restrict__ leaf_src) {
+                                                 const uint4* __restrict__ paux, RenderRec* __restrict__ rout,
+                                                 float* __restrict__ shout, float* __restrict__ bout,
+                                                 uint32_t* __restrict__ leaf_src, uint4* __restrict__ aux) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m) return;
-    const uint32_t s = perm[j];
+    const uint32_t t = perm[j];
+    const uint4 pa = paux ? paux[t] : make_uint4(t, 0xFFFFFFFFu, 0u, 0u);
+    const uint32_t s = pa.x;
     rout[j] = rin[s];
-    const float4* si = reinterpret_cast<const float4*>(shin + 48ull * s);
-    float4* so = reinterpret_cast<float4*>(shout + 48ull * j);
+    if (shout) {
+        const float4* si = reinterpret_cast<const float4*>(shin + 48ull * s);
+        float4* so = reinterpret_cast<float4*>(shout + 48ull * j);
 #pragma unroll
-    for (int k = 0; k < 12; ++k) so[k] = si[k];
+        for (int k = 0; k < 12; ++k) so[k] = si[k];
+    }
 #pragma unroll
-    for (int k = 0; k < 6; ++k) bout[6 * j + k] = bin[6ull * s + k];
+    for (int k = 0; k < 6; ++k) bout[6 * j + k] = bin[6ull * t + k];
     leaf_src[j] = s;
+    if (aux) aux[j] = pa;
+}
+
+// ---- SplitBLAS analogue (SplitBLAS.cpp:91-186): proxies split into grid-cell pieces
+struct Grid {
+    float mn[3];
+    float inv;   // 1 / cell size
+    float size;  // cell size
+    uint32_t n[3];
+};
+__device__ inline int grid_cell(const Grid& g, int a, float x) {
+    const int i = (int)floorf((x - g.mn[a]) * g.inv);
+    return i < 0 ? 0 : (i >= (int)g.n[a] ? (int)g.n[a] - 1 : i);
+}
+
+__global__ __launch_bounds__(256) void k_piece_count(uint64_t m, const float* __restrict__ boxes, Grid g,
+                                                     uint64_t* __restrict__ cnt) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > m) return;
+    if (i == m) {
+        cnt[i] = 0;
+        return;
+    }
+    uint64_t c = 1;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) c *= (uint64_t)(grid_cell(g, a, boxes[6 * i + 3 + a]) - grid_cell(g, a, boxes[6 * i + a]) + 1);
+    cnt[i] = c;
+}
+
+__device__ inline uint32_t pack_cell(int x, int y, int z) { return (uint32_t)x | ((uint32_t)y << 10) | ((uint32_t)z << 20); }
+
+// One piece per overlapped cell: box = proxy box clipped to the cell, padded so that a crossing point
+// the render kernel assigns to the cell is inside it.  aux = {proxy, cell, proxy's lowest cell,
+// highest cell} (cells packed 10 bits per axis); the render kernel admits a crossing in the piece
+// whose cell holds the crossing point (clamped to the proxy's cell range), so every crossing of the
+// proxy is taken exactly once — the analogue of the reference's triangle clipping, where a ray
+// crosses a clipped triangle only inside its cell.  A proxy inside one cell keeps its box and cell
+// "any" (0xFFFFFFFF: no point test).
+__global__ __launch_bounds__(256) void k_piece_emit(uint64_t m, const float* __restrict__ boxes, Grid g,
+                                                    const uint64_t* __restrict__ off, float* __restrict__ pbox,
+                                                    uint4* __restrict__ paux) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    int lo[3], hi[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = grid_cell(g, a, boxes[6 * i + a]);
+        hi[a] = grid_cell(g, a, boxes[6 * i + 3 + a]);
+    }
+    uint64_t p = off[i];
+    const bool single = lo[0] == hi[0] && lo[1] == hi[1] && lo[2] == hi[2];
+    const uint32_t plo = pack_cell(lo[0], lo[1], lo[2]), phi = pack_cell(hi[0], hi[1], hi[2]);
+    for (int iz = lo[2]; iz <= hi[2]; ++iz)
+        for (int iy = lo[1]; iy <= hi[1]; ++iy)
+            for (int ix = lo[0]; ix <= hi[0]; ++ix, ++p) {
+                const int ci[3] = {ix, iy, iz};
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    const float bl = boxes[6 * i + a], bh = boxes[6 * i + 3 + a];
+                    if (single) {
+                        pbox[6 * p + a] = bl;
+                        pbox[6 * p + 3 + a] = bh;
+                        continue;
+                    }
+                    const float cl = g.mn[a] + (float)ci[a] * g.size, ch = g.mn[a] + (float)(ci[a] + 1) * g.size;
+                    const float pad = 1e-5f * g.size + 1e-6f * fmaxf(fabsf(cl), fabsf(ch));
+                    pbox[6 * p + a] = fmaxf(bl, cl - pad);
+                    pbox[6 * p + 3 + a] = fminf(bh, ch + pad);
+                }
+                paux[p] = make_uint4((uint32_t)i, single ? 0xFFFFFFFFu : pack_cell(ix, iy, iz), plo, phi);
+            }
 }
 
 // Range-union sparse table over the leaf boxes (leaf order): level k holds, for every i, the union of
@@ -397,29 +479,28 @@ __global__ void k_level_advance(uint32_t* ctl) {
 
 }  // namespace
 
-gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
-    const int64_t m = (int64_t)c->m;
+gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap) {
+    const int64_t mp = (int64_t)c->m;  // proxies (survivors)
     gvrt_dfree(c, (void**)&c->d_recs);
     gvrt_dfree(c, (void**)&c->d_sh);
     gvrt_dfree(c, (void**)&c->d_nodes);
     gvrt_dfree(c, (void**)&c->d_nodes4);
     gvrt_dfree(c, (void**)&c->d_leaf_src);
+    gvrt_dfree(c, (void**)&c->d_leaf_aux);
     c->n_nodes4 = 0;
+    c->n_leaves = 0;
+    c->split_cells = 0;
     c->accel = false;
     c->depth = 0;
-    if (m == 0) {
+    if (mp == 0) {
         c->accel = true;
         c->stats.bvh_nodes = 0;
+        c->stats.bvh_leaves = 0;
         c->stats.bvh_depth = 0;
         return GVRT_OK;
     }
-    if (m > 0x7FFFFFFFll) return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "more than 2^31-1 survivors");
+    if (mp > 0x7FFFFFFFll) return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "more than 2^31-1 survivors");
     gvrt_status s;
-    const int64_t ninternal = m > 1 ? m - 1 : 1;
-    if ((s = gvrt_dalloc(c, (void**)&c->d_recs, sizeof(RenderRec) * m))) return s;
-    if ((s = gvrt_dalloc(c, (void**)&c->d_sh, 192ull * m))) return s;
-    if ((s = gvrt_dalloc(c, (void**)&c->d_nodes, sizeof(BvhNode) * ninternal))) return s;
-    if ((s = gvrt_dalloc(c, (void**)&c->d_leaf_src, 4ull * m))) return s;
 
     // scratch
     uint32_t *bnd = nullptr, *vals = nullptr, *vals2 = nullptr, *dep = nullptr;
@@ -429,6 +510,10 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
     int32_t *lpar = nullptr, *npar = nullptr;
     float* lboxes = nullptr;
     void* tmp = nullptr;
+    float* pbox = nullptr;  // split pieces
+    uint4* paux = nullptr;
+    uint64_t *pcnt = nullptr, *poff = nullptr;
+    void* ptmp = nullptr;
     auto cleanup = [&]() {
         gvrt_dfree(c, (void**)&bnd);
         gvrt_dfree(c, (void**)&keys);
@@ -443,6 +528,11 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
         gvrt_dfree(c, (void**)&npar);
         gvrt_dfree(c, (void**)&lboxes);
         gvrt_dfree(c, &tmp);
+        gvrt_dfree(c, (void**)&pbox);
+        gvrt_dfree(c, (void**)&paux);
+        gvrt_dfree(c, (void**)&pcnt);
+        gvrt_dfree(c, (void**)&poff);
+        gvrt_dfree(c, &ptmp);
     };
 #define TRY(x)                   \
     do {                         \
@@ -459,6 +549,73 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
             return gvrt_hip_check(c, _e, what);         \
         }                                               \
     } while (0)
+
+    // ---- optional split into grid-cell pieces (SplitBLAS analogue): the BVH leaves become pieces
+    int64_t m = mp;  // leaves
+    const float* boxes_in = c->d_boxes_c;
+    if (ap.split_cells > 0) {
+        const unsigned pb = (unsigned)((mp + 255) / 256), prb = pb < 1024 ? pb : 1024;
+        TRY(gvrt_dalloc(c, (void**)&bnd, 32));
+        TRY(gvrt_dalloc(c, (void**)&bpart, 24ull * prb));
+        const uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
+        TRYH(hipMemcpyAsync(bnd, init, 24, hipMemcpyHostToDevice, c->stream), "bounds init");
+        hipLaunchKernelGGL(k_bounds<false>, dim3(prb), dim3(256), 0, c->stream, (uint64_t)mp, c->d_boxes_c, bpart);
+        hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(256), 0, c->stream, prb, bpart, bnd);
+        uint32_t hb[6];
+        TRYH(hipMemcpyAsync(hb, bnd, 24, hipMemcpyDeviceToHost, c->stream), "scene box");
+        TRYH(hipStreamSynchronize(c->stream), "sync");
+        // grid of SplitBLAS.cpp:103-112: SCENE_EPSILON 1e-4 margins, N cells on the longest axis
+        Grid g{};
+        float size[3], maxs = 0.0f;
+        for (int a = 0; a < 3; ++a) {
+            g.mn[a] = ord2f(hb[a]) - 1e-4f;
+            size[a] = (ord2f(hb[3 + a]) + 1e-4f) - g.mn[a];
+            maxs = size[a] > maxs ? size[a] : maxs;
+        }
+        g.size = maxs / (float)ap.split_cells;
+        g.inv = 1.0f / g.size;
+        for (int a = 0; a < 3; ++a)
+            g.n[a] = size[a] == maxs ? ap.split_cells : (uint32_t)(size[a] / g.size) + 1u;
+        TRY(gvrt_dalloc(c, (void**)&pcnt, 8ull * (mp + 1)));
+        TRY(gvrt_dalloc(c, (void**)&poff, 8ull * (mp + 1)));
+        hipLaunchKernelGGL(k_piece_count, dim3((unsigned)((mp + 1 + 255) / 256)), dim3(256), 0, c->stream, (uint64_t)mp,
+                           c->d_boxes_c, g, pcnt);
+        size_t pt = 0;
+        TRYH(hipcub::DeviceScan::ExclusiveSum(nullptr, pt, pcnt, poff, (int)(mp + 1), c->stream), "scan size");
+        TRY(gvrt_dalloc(c, &ptmp, pt ? pt : 16));
+        TRYH(hipcub::DeviceScan::ExclusiveSum(ptmp, pt, pcnt, poff, (int)(mp + 1), c->stream), "scan");
+        uint64_t np = 0;
+        TRYH(hipMemcpyAsync(&np, poff + mp, 8, hipMemcpyDeviceToHost, c->stream), "pieces");
+        TRYH(hipStreamSynchronize(c->stream), "sync");
+        if (np == 0 || np > (1ull << 27)) {  // (memory: ~300 B of build scratch per piece)
+            cleanup();
+            return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "split produced an unsupported number of pieces");
+        }
+        m = np;
+        TRY(gvrt_dalloc(c, (void**)&pbox, 24ull * m));
+        TRY(gvrt_dalloc(c, (void**)&paux, 16ull * m));
+        hipLaunchKernelGGL(k_piece_emit, dim3(pb), dim3(256), 0, c->stream, (uint64_t)mp, c->d_boxes_c, g, poff, pbox,
+                           paux);
+        TRYH(hipGetLastError(), "k_piece_emit");
+        boxes_in = pbox;
+        c->split_cells = ap.split_cells;
+        for (int a = 0; a < 3; ++a) {
+            c->grid_min[a] = g.mn[a];
+            c->grid_n[a] = g.n[a];
+        }
+        c->grid_inv = g.inv;
+        gvrt_dfree(c, (void**)&bnd);
+        gvrt_dfree(c, (void**)&bpart);
+    }
+    c->n_leaves = (uint64_t)m;
+
+    const int64_t ninternal = m > 1 ? m - 1 : 1;
+    TRY(gvrt_dalloc(c, (void**)&c->d_recs, sizeof(RenderRec) * m));
+    if (!c->split_cells) TRY(gvrt_dalloc(c, (void**)&c->d_sh, 192ull * m));
+    else TRY(gvrt_dalloc(c, (void**)&c->d_leaf_aux, 16ull * m));
+    TRY(gvrt_dalloc(c, (void**)&c->d_nodes, sizeof(BvhNode) * ninternal));
+    TRY(gvrt_dalloc(c, (void**)&c->d_leaf_src, 4ull * m));
+
     TRY(gvrt_dalloc(c, (void**)&bnd, 32));
     TRY(gvrt_dalloc(c, (void**)&keys, 8ull * m));
     TRY(gvrt_dalloc(c, (void**)&vals, 4ull * m));
@@ -489,14 +646,15 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
     TRYH(hipEventRecord(c->ev0, c->stream), "event");
     const uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
     TRYH(hipMemcpyAsync(bnd, init, 24, hipMemcpyHostToDevice, c->stream), "bounds init");
-    hipLaunchKernelGGL(k_bounds, dim3(rblocks), dim3(256), 0, c->stream, (uint64_t)m, c->d_boxes_c, bpart);
+    hipLaunchKernelGGL(k_bounds<true>, dim3(rblocks), dim3(256), 0, c->stream, (uint64_t)m, boxes_in, bpart);
     hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(256), 0, c->stream, rblocks, bpart, bnd);
-    hipLaunchKernelGGL(k_morton, dim3(blocks), dim3(256), 0, c->stream, (uint64_t)m, c->d_boxes_c, bnd, keys, vals);
+    hipLaunchKernelGGL(k_morton, dim3(blocks), dim3(256), 0, c->stream, (uint64_t)m, boxes_in, bnd, keys, vals);
     TRYH(hipGetLastError(), "k_morton");
     TRYH(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys2, vals, vals2, (int)m, 0, 63, c->stream),
          "SortPairs");
     hipLaunchKernelGGL(k_permute, dim3(blocks), dim3(256), 0, c->stream, (uint64_t)m, vals2, c->d_recs_c, c->d_sh48,
-                       c->d_boxes_c, c->d_recs, c->d_sh, lboxes, c->d_leaf_src);
+                       boxes_in, paux, c->d_recs, c->d_sh, lboxes, c->d_leaf_src,
+                       reinterpret_cast<uint4*>(c->d_leaf_aux));
     TRYH(hipGetLastError(), "k_permute");
     if (m == 1) {
         // single proxy: one 4-wide root with one leaf slot
@@ -522,7 +680,7 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
     } else {
         TRYH(hipMemsetAsync(dep, 0, 4, c->stream), "memset");
         const char* be = getenv("GVRT_BUILDER");
-        const bool ploc = be && be[0] == 'p';  // "ploc": measured 3 % slower to render (more visits), see DESIGN.md
+        const bool ploc = ap.builder == 1 || (be && be[0] == 'p');  // "ploc": measured 3 % slower to render (more visits), see DESIGN.md
         int32_t root = 0;
         if (ploc) {
             uint32_t iters = 0;
@@ -609,6 +767,7 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c) {
     if ((BVH_W - 1) * c->depth4 + 2 > (uint32_t)STACK_DEPTH)
         return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "LBVH deeper than the render kernel's traversal stack");
     c->stats.bvh_nodes = c->n_nodes4;
+    c->stats.bvh_leaves = c->n_leaves;
     c->stats.bvh_depth = c->depth;
     c->accel = true;
     return GVRT_OK;

@@ -243,6 +243,22 @@ __device__ inline bool particle_alpha(f3 ok, f3 dk, float l2, float density, flo
 // (particlePrimitives.comp:76-79 vertices; their face planes).  Per slab the crossing interval is
 // centre m = -(n . ok) / (n . dk) +- hk / |n . dk|; the reciprocal is clamped to +-1e30 so a ray
 // parallel to a slab gives an unbounded interval when inside it and an empty one when outside.
+// Cell of the crossing point o + t d (grid of gvrt_lbvh.hip's k_piece_emit), each axis clamped to
+// the proxy's cell range [lo, hi] so that every crossing maps to one of the proxy's pieces; packed 10
+// bits per axis.  Every piece of a proxy evaluates the same expression on the same record, so a
+// crossing is admitted by exactly one piece.
+__device__ inline uint32_t crossing_cell(f3 o, f3 d, float t, const RenderArgs& a, uint32_t lo, uint32_t hi) {
+    const float p[3] = {fmaf(t, d.x, o.x), fmaf(t, d.y, o.y), fmaf(t, d.z, o.z)};
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int l = (int)((lo >> (10 * k)) & 1023u), h = (int)((hi >> (10 * k)) & 1023u);
+        const int i = (int)floorf((p[k] - a.grid_min[k]) * a.grid_inv);
+        c |= (uint32_t)(i < l ? l : (i > h ? h : i)) << (10 * k);
+    }
+    return c;
+}
+
 __device__ inline void ico_clip(f3 ok, f3 dk, float hk, float& tn, float& tf) {
     float lo = -INFINITY, hi = INFINITY;
     // one slab at a time (short live ranges: this runs with the whole k-buffer in registers)
@@ -309,7 +325,8 @@ __device__ inline float unif(float v) { return __int_as_float(__builtin_amdgcn_r
 
 template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK>
 __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const RenderArgs a, const Bvh4Node* __restrict__ nodes_,
-                                                const RenderRec* __restrict__ recs_, const float* __restrict__ sh_,
+                                                const RenderRec* __restrict__ recs_, const RenderRec* __restrict__ crecs_,
+                                                const uint4* __restrict__ aux_, const float* __restrict__ sh_,
                                                 const float* __restrict__ view_inv_, const uint32_t* __restrict__ tiles_,
                                                 uint8_t* __restrict__ rgba8_, float* __restrict__ rgba32f_,
                                                 float* __restrict__ ray_dirs_, uint32_t* __restrict__ hit_counts_,
@@ -537,8 +554,11 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                 const uint64_t bk = GVRT_PICK(bal, k);
                 const int32_t ck = GVRT_PICK(ch, k);
                 const RenderRec rec = recs_[~ck];
+                // split (SplitBLAS analogue): the piece's proxy id and cell; cell == ~0u admits every crossing
+                uint4 pa = make_uint4((uint32_t)(~ck), 0xFFFFFFFFu, 0u, 0u);
+                if (aux_) pa = aux_[~ck];
                 {
-                    const uint32_t gi = uni((uint32_t)(~ck));
+                    const uint32_t gi = uni(pa.x);
                     if constexpr (STATS) ++w_leaves;
                     if (__builtin_amdgcn_inverse_ballot_w64(bk)) {  // exec &= bk: no per-lane bit test
                         if constexpr (STATS) ++l_leaves;
@@ -561,8 +581,12 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                             ico_clip(ok, dk, hk, tn, tf);
                             if (tn <= tf) {
                                 const float al = acc ? galpha : -1.0f;
-                                const bool in0 = (a.tmin_inclusive ? tn >= tlo : tn > tlo) && tn <= thi;
-                                const bool in1 = (a.tmin_inclusive ? tf >= tlo : tf > tlo) && tf <= thi;
+                                bool in0 = (a.tmin_inclusive ? tn >= tlo : tn > tlo) && tn <= thi;
+                                bool in1 = (a.tmin_inclusive ? tf >= tlo : tf > tlo) && tf <= thi;
+                                if (uni(pa.y) != 0xFFFFFFFFu) {
+                                    in0 = in0 && crossing_cell(o, d, tn, a, pa.z, pa.w) == pa.y;
+                                    in1 = in1 && crossing_cell(o, d, tf, a, pa.z, pa.w) == pa.y;
+                                }
                                 const float ta = in0 && tn < tcut ? tn : (in1 && tf < tcut ? tf : INF_DIST);
                                 const float tb = (in0 && in1 && tf < tcut) ? tf : INF_DIST;
                                 if (ta < kt[KB - 1]) {
@@ -644,7 +668,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
 #endif
                         if constexpr (PACK) {
                             // processHit re-evaluates the response of the hit particle (per-lane record load)
-                            const RenderRec rec = recs_[hid];
+                            const RenderRec rec = crecs_[hid];
                             f3 ok, dk;
                             kernel_frame(rec, o, d, ok, dk);
                             const float l2 = len2(dk);
@@ -774,7 +798,7 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
     const dim3 g((unsigned)blocks), b(256);
     // every pointer is its own __restrict__ argument: the uniform node / record loads can then be
     // proven unclobbered by the output stores and are emitted as scalar (s_load) loads
-#define KARGS a.nodes, a.recs, a.sh, a.view_inv, a.tiles, a.rgba8, a.rgba32f, a.ray_dirs, a.hit_counts, a.stats
+#define KARGS a.nodes, a.recs, a.crecs, a.aux, a.sh, a.view_inv, a.tiles, a.rgba8, a.rgba32f, a.ray_dirs, a.hit_counts, a.stats
 #define GVRT_LAUNCH(L, A, K, P)                                                                    \
     do {                                                                                           \
         if (a.stats) hipLaunchKernelGGL((k_render<L, A, K, true, P>), g, b, 0, c->stream, a, KARGS);  \

@@ -116,6 +116,7 @@ typedef struct {
     uint64_t phase_cycles[4];   /* s_memtime cycles summed over waves (stats enabled): node visits,
                                    leaf tests + k-buffer insertion, compositing, whole kernel */
     uint64_t wave_dead_visits;  /* node visits in which no lane hit any child box */
+    uint64_t bvh_leaves;        /* BVH leaves: the survivors, or their grid-cell pieces when split */
 } gvrt_stats;
 
 /* --------------------------------------------------------------------------------------- */
@@ -147,9 +148,24 @@ gvrt_status gvrt_build_enclosing(gvrt_handle h, const gvrt_enclosing_params* p, 
 gvrt_status gvrt_read_enclosing(gvrt_handle h, float* density12, float* sh48, float* verts36,
                                 uint32_t* tris60, uint32_t* src_index);
 
+/* Acceleration-structure options.  split_cells > 0 is the SplitBLAS analogue (SPLIT_BLAS,
+ * base/Define.h:45-47; projects/VulkanFullRT/SplitBLAS.cpp:91-186): a grid of split_cells cells on
+ * the scene's longest axis (the reference uses NUMBER_OF_CELLS_PER_LONGEST_AXIS = 10), every proxy
+ * split into one piece per grid cell its box overlaps, each piece admitting only the crossings whose
+ * point lies in its cell (so every crossing is found exactly once).  split_cells <= 1023 (0: no
+ * split).  builder: 0 Karras LBVH, 1 PLOC. */
+typedef struct {
+    uint32_t split_cells;
+    uint32_t builder;
+    uint32_t reserved[6];
+} gvrt_accel_params;
+
+void gvrt_default_accel_params(gvrt_accel_params* p);
+
 /* createBottomLevel/TopLevelAccelerationStructure3DGRT (VulkanFullRT.cpp:575-787):
- * LBVH (Morton codes, radix sort, Karras hierarchy, AABB refit) over the proxies. */
+ * BVH over the proxies (Morton codes, radix sort, Karras hierarchy, 4-wide collapse). */
 gvrt_status gvrt_build_accel(gvrt_handle h);
+gvrt_status gvrt_build_accel_ex(gvrt_handle h, const gvrt_accel_params* p);
 
 /* Particle Rendering pass: buildCommandBuffer (VulkanFullRT.cpp:1185-1244) dispatching
  * raygen/anyhit (RT) or particleRendering.comp (RQ), and the light-field launch

@@ -18,7 +18,7 @@ waves = (W + 7) // 8 * ((H + 7) // 8)
 rays = W * H
 out = {}
 with gv.Renderer(0) as r:
-    r.prepare(s)
+    r.prepare(s, split_cells=int(os.environ.get("DIAG_SPLIT", "0")))
     runs = [("literal", gv.MODE_LITERAL, 0)] + [(f"fast_k{k}", gv.MODE_FAST, k) for k in depths]
     for name, mode, k in runs:
         kw = dict(mode=mode, kbuffer_depth=k, rgba8=False, rgba32f=False)
@@ -38,7 +38,7 @@ with gv.Renderer(0) as r:
                      "node_visits/wave": round(st["wave_node_visits"] / waves, 1),
                      "leaf_visits/wave": round(st["wave_leaf_visits"] / waves, 1),
                      "dead_visits/wave": round(st["wave_dead_visits"] / waves, 1),
-                     "lane_leaf_tests/ray": round(st["lane_leaf_tests"] / rays, 2), "bvh_depth": st["bvh_depth"], "bvh_nodes": st["bvh_nodes"], "accel_ms": round(st["accel_ms"], 2)}
+                     "lane_leaf_tests/ray": round(st["lane_leaf_tests"] / rays, 2), "bvh_depth": st["bvh_depth"], "bvh_nodes": st["bvh_nodes"], "bvh_leaves": st["bvh_leaves"], "accel_ms": round(st["accel_ms"], 2)}
         pc = st["phase_cycles"]
         if pc[3]:
             out[name]["phase_frac"] = {"node": round(pc[0] / pc[3], 3), "leaf+insert": round(pc[1] / pc[3], 3),

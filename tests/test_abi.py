@@ -32,7 +32,8 @@ def test_every_declared_symbol_is_exported(gv):
 
 
 STRUCTS = {"gvrt_splats": "Splats", "gvrt_enclosing_params": "EnclosingParams", "gvrt_render_params": "RenderParams",
-           "gvrt_tile": "Tile", "gvrt_image": "Image", "gvrt_stats": "Stats", "gvrt_splat_buffers": "SplatBuffers"}
+           "gvrt_tile": "Tile", "gvrt_image": "Image", "gvrt_stats": "Stats", "gvrt_splat_buffers": "SplatBuffers",
+           "gvrt_accel_params": "AccelParams"}
 
 
 def test_struct_layouts_match_header(gv):
