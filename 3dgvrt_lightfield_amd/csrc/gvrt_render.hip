@@ -306,11 +306,47 @@ __device__ inline int32_t writelane(int32_t old, int32_t v, int32_t lane) {
 // arr[k] for a wave-uniform k: a select chain (s_cmp / s_cselect) over the register array.  A macro,
 // not a function taking the array by reference: that form pushed the arrays to scratch (+55 % time).
 #if GVRT_BVH_W == 4
-#define GVRT_PICK(a, k) ((k) == 0 ? (a)[0] : (k) == 1 ? (a)[1] : (k) == 2 ? (a)[2] : (a)[3])
+template <typename T>
+__device__ inline T sel4(T a0, T a1, T a2, T a3, uint32_t k) {  // values, not an array: stays s_cselect
+    const T lo = (k & 1u) ? a1 : a0, hi = (k & 1u) ? a3 : a2;
+    return (k & 2u) ? hi : lo;
+}
+#define GVRT_PICK(a, k) sel4((a)[0], (a)[1], (a)[2], (a)[3], (uint32_t)(k))
 #else
 #define GVRT_PICK(a, k)                                                                                  \
     ((k) == 0 ? (a)[0] : (k) == 1 ? (a)[1] : (k) == 2 ? (a)[2] : (k) == 3 ? (a)[3] : (k) == 4 ? (a)[4] \
      : (k) == 5 ? (a)[5] : (k) == 6 ? (a)[6] : (a)[7])
+#endif
+
+// Node fetch.  The compiler splits a 128-B node into dwordx16 + dwordx8 + dwordx4 + dword loads with
+// lgkmcnt waits between them (three dependent scalar round trips per node visit); GVRT_ASM_NODE issues
+// the two s_load_dwordx16 back to back and waits once.
+#ifndef GVRT_ASM_NODE
+#define GVRT_ASM_NODE 1
+#endif
+#if GVRT_ASM_NODE && GVRT_BVH_W == 4
+typedef int32_t sv16 __attribute__((ext_vector_type(16)));
+struct NodeS {
+    sv16 a, b;  // dwords 0..15, 16..31 of a Bvh4Node
+    __device__ int32_t w(int i) const { return i < 16 ? a[i] : b[i - 16]; }
+    __device__ float f(int i) const { return __int_as_float(w(i)); }
+};
+__device__ inline NodeS load_node(const Bvh4Node* __restrict__ p) {
+    NodeS n;
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(n.a), "=&s"(n.b)
+                 : "s"(p));
+    return n;
+}
+#define NODE_BOX(nd, k, j) (nd).f(6 * (k) + (j))
+#define NODE_CHILD(nd, k) (nd).w(24 + (k))
+#define NODE_PAD(nd, j) (nd).w(29 + (j))
+#else
+typedef Bvh4Node NodeS;
+__device__ inline NodeS load_node(const Bvh4Node* __restrict__ p) { return *p; }
+#define NODE_BOX(nd, k, j) (nd).box[k][j]
+#define NODE_CHILD(nd, k) (nd).child[k]
+#define NODE_PAD(nd, j) (nd).pad[j]
 #endif
 
 __device__ inline uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -489,8 +525,10 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
         float tcut = INF_DIST;  // termination-aware cull distance of this lane (see the leaf insert)
         const uint64_t amask = __builtin_amdgcn_ballot_w64(active);
         sp = 0;
-        Bvh4Node nd = nodes_[0];  // whole node: scalar loads (2x s_load_dwordx16 when 4-wide)
+        int32_t cur = 0;  // node index (wave-uniform); the node is fetched at the top of each visit so its
+                          // 32 SGPRs are not loop-carried
         while (true) {
+            const NodeS nd = load_node(nodes_ + unii(cur));  // whole node: 2x s_load_dwordx16 (4-wide)
             [[maybe_unused]] uint64_t t_node0 = 0;
             if constexpr (STATS) {
                 ++w_nodes;
@@ -502,17 +540,17 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
             // (a per-octant min/max-free box test measured within noise: +0.7 %, 9 code copies)
 #pragma unroll
             for (int k = 0; k < BVH_W; ++k) {
-                const float* cb = nd.box[k];
-#if GVRT_PK_BOX
-                const bool hit = box_hit_pk(cb, oinv, inv, tlo, tc, ent[k]);
+#if GVRT_PK_BOX && !GVRT_ASM_NODE
+                const bool hit = box_hit_pk(nd.box[k], oinv, inv, tlo, tc, ent[k]);
 #else
-                const bool hit = box_hit(cb[0], cb[2], cb[4], cb[1], cb[3], cb[5], o, oinv, inv, tlo, tc, ent[k]);
+                const bool hit = box_hit(NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 1),
+                                         NODE_BOX(nd, k, 3), NODE_BOX(nd, k, 5), o, oinv, inv, tlo, tc, ent[k]);
 #endif
                 bal[k] = __builtin_amdgcn_ballot_w64(hit) & amask;  // compare result straight to an SGPR mask
             }
             int32_t ch[BVH_W];
 #pragma unroll
-            for (int k = 0; k < BVH_W; ++k) ch[k] = unii(nd.child[k]);
+            for (int k = 0; k < BVH_W; ++k) ch[k] = unii(NODE_CHILD(nd, k));
             // ---- children in the node's stored order (in-order of the binary split), forward when the
             // first lane's ray points along +axis, else backward: a handful of SALU ops per node
             // (the entry-distance sort below costs ~100)
@@ -520,13 +558,13 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
 #pragma unroll
             for (int k = 0; k < BVH_W; ++k) hm |= bal[k] ? (1u << k) : 0u;
             if constexpr (STATS) w_dead += hm == 0 ? 1u : 0u;
-            const uint32_t inner = uni(nd.pad[1]);
+            const uint32_t inner = uni(NODE_PAD(nd, 1));
             uint32_t leafmask = hm & ~inner;
             uint32_t im = hm & inner;
             int32_t next = -1;
             auto chsel = [&](int k) { return GVRT_PICK(ch, k); };
             if (im) {
-                const bool rev = (rsign >> uni(nd.pad[0])) & 1u;
+                const bool rev = (rsign >> uni(NODE_PAD(nd, 0))) & 1u;
                 const int first = rev ? 31 - __clz(im) : __ffs(im) - 1;
                 next = chsel(first);
                 im &= ~(1u << first);
@@ -633,7 +671,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
             }
             if constexpr (STATS) cyc_leaf += __builtin_amdgcn_s_memtime() - t_leaf0;
             if (next < 0) break;
-            nd = nodes_[unii(next)];  // uniform by construction; readfirstlane lets the compiler see it
+            cur = next;  // uniform by construction; readfirstlane at the load lets the compiler see it
         }
 
         // ---------------- process k hits (particleRendering.comp:153-187)
