@@ -71,7 +71,7 @@ class Stats(C.Structure):
                 ("pad1", C.c_float), ("device_bytes", C.c_uint64), ("wave_node_visits", C.c_uint64),
                 ("wave_leaf_visits", C.c_uint64), ("lane_leaf_tests", C.c_uint64),
                 ("phase_cycles", C.c_uint64 * 4), ("wave_dead_visits", C.c_uint64),
-                ("bvh_leaves", C.c_uint64)]
+                ("bvh_leaves", C.c_uint64), ("wave_rounds", C.c_uint64), ("wave_late_node_visits", C.c_uint64)]
 
 
 H = C.c_void_p

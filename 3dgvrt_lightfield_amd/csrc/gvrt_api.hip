@@ -373,7 +373,7 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
         }
     }
     if (c->stats_on) {
-        GVRT_HIP(c, hipMemsetAsync(c->d_stats, 0, 88, c->stream));
+        GVRT_HIP(c, hipMemsetAsync(c->d_stats, 0, 104, c->stream));
         a.stats = c->d_stats;
     }
     GVRT_HIP(c, hipEventRecord(c->ev0, c->stream));
@@ -385,8 +385,8 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
         if (bhc) GVRT_HIP(c, hipMemcpyAsync(out->hit_counts, a.hit_counts, bhc, hipMemcpyDeviceToHost, c->stream));
         if (b8) GVRT_HIP(c, hipMemcpyAsync(out->rgba8, a.rgba8, b8, hipMemcpyDeviceToHost, c->stream));
     }
-    unsigned long long hs[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (c->stats_on) GVRT_HIP(c, hipMemcpyAsync(hs, c->d_stats, 88, hipMemcpyDeviceToHost, c->stream));
+    unsigned long long hs[13] = {};
+    if (c->stats_on) GVRT_HIP(c, hipMemcpyAsync(hs, c->d_stats, 104, hipMemcpyDeviceToHost, c->stream));
     GVRT_HIP(c, hipStreamSynchronize(c->stream));
     float ms = 0.f;
     GVRT_HIP(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
@@ -400,6 +400,8 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
     c->stats.lane_leaf_tests = hs[5];
     for (int k = 0; k < 4; ++k) c->stats.phase_cycles[k] = hs[6 + k];
     c->stats.wave_dead_visits = hs[10];
+    c->stats.wave_rounds = hs[11];
+    c->stats.wave_late_node_visits = hs[12];
     return GVRT_OK;
 }
 

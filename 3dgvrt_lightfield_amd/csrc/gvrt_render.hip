@@ -446,6 +446,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
     // STATS phase timers (s_memtime, wave-uniform): node visits, leaves + insertion, composite
     uint64_t cyc_node = 0, cyc_leaf = 0, cyc_comp = 0;
     uint32_t w_dead = 0;  // node visits where no lane hits any child box
+    uint32_t w_rounds = 0, w_late = 0;  // traversal rounds of this wave; node visits after the first round
     [[maybe_unused]] const uint64_t cyc_start = STATS ? __builtin_amdgcn_s_memtime() : 0;
     bool active = valid && a.nrecs > 0 && (fmaxf(0.0f, tminb - EPS_T) <= tmaxb) && (1.0f > a.min_transmittance);
 
@@ -527,13 +528,15 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
         sp = 0;
         int32_t cur = 0;  // node index (wave-uniform); the node is fetched at the top of each visit so its
                           // 32 SGPRs are not loop-carried
+        if constexpr (STATS) ++w_rounds;
         while (true) {
-            const NodeS nd = load_node(nodes_ + unii(cur));  // whole node: 2x s_load_dwordx16 (4-wide)
             [[maybe_unused]] uint64_t t_node0 = 0;
             if constexpr (STATS) {
                 ++w_nodes;
-                t_node0 = __builtin_amdgcn_s_memtime();
+                w_late += w_rounds > 1 ? 1u : 0u;
+                t_node0 = __builtin_amdgcn_s_memtime();  // the node phase includes the fetch
             }
+            const NodeS nd = load_node(nodes_ + unii(cur));  // whole node: 2x s_load_dwordx16 (4-wide)
             const float tc = fminf(fminf(thi, kt[KB - 1]), tcut);
             float ent[BVH_W];
             uint64_t bal[BVH_W];
@@ -809,6 +812,8 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
             atomicAdd(stats_ + 8, (unsigned long long)cyc_comp);
             atomicAdd(stats_ + 9, (unsigned long long)(__builtin_amdgcn_s_memtime() - cyc_start));
             atomicAdd(stats_ + 10, (unsigned long long)w_dead);
+            atomicAdd(stats_ + 11, (unsigned long long)w_rounds);
+            atomicAdd(stats_ + 12, (unsigned long long)w_late);
         }
     }
 }

@@ -117,6 +117,8 @@ typedef struct {
                                    leaf tests + k-buffer insertion, compositing, whole kernel */
     uint64_t wave_dead_visits;  /* node visits in which no lane hit any child box */
     uint64_t bvh_leaves;        /* BVH leaves: the survivors, or their grid-cell pieces when split */
+    uint64_t wave_rounds;       /* traversal rounds summed over waves (stats enabled) */
+    uint64_t wave_late_node_visits; /* node visits in the second and later rounds of a wave */
 } gvrt_stats;
 
 /* --------------------------------------------------------------------------------------- */
