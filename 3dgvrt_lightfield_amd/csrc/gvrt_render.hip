@@ -54,6 +54,10 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 #ifndef GVRT_SH_PREFETCH
 #define GVRT_SH_PREFETCH 1
 #endif
+// composite: slots per group (static register indices within a group; one buffer shift per group)
+#ifndef GVRT_COMP_UNROLL
+#define GVRT_COMP_UNROLL 4
+#endif
 #ifndef GVRT_TCUT
 #define GVRT_TCUT 1
 #endif
@@ -686,17 +690,21 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                 float T = s_T[wid][lane];
                 float4 acc = s_acc[wid][lane];
                 float last = s_last[wid][lane];
-                // rolled loop over slots: composite slot 0, then shift the buffer down by one
+                // Slots in groups of CU (static indices inside a group, so no per-hit register shift);
+                // the buffer shifts down by CU between groups.  Per lane: stop at the first empty slot
+                // or once T <= minTransmittance (slots are sorted with the empty ones last, T only falls).
+                bool go = true;
 #pragma unroll 1
-                for (int it = 0; it < KB; ++it) {
-                    // slots are sorted with the empty ones last, and T only falls: this lane is done
-                    if (!(kid[0] != INVALID_ID && T > a.min_transmittance)) break;
-                    {
+                for (int base = 0; base < KB; base += GVRT_COMP_UNROLL) {
+#pragma unroll
+                    for (int j = 0; j < GVRT_COMP_UNROLL; ++j) {
+                        go = go && kid[j] != INVALID_ID && T > a.min_transmittance;
+                        if (!go) continue;
                         if constexpr (STATS) ++nproc;
                         uint32_t hid;
                         float halpha;
                         bool hacc;
-                        hid = PACK ? (kid[0] >> 8) : kid[0];
+                        hid = PACK ? (kid[j] >> 8) : kid[j];
 #if GVRT_SH_PREFETCH
                         // the SH address needs only the id: issue all 12 loads with the record's, one
                         // memory round trip per hit instead of one per dependent chunk
@@ -704,7 +712,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                         {
                             const float4* s4 = reinterpret_cast<const float4*>(sh_ + 48ull * hid);
 #pragma unroll
-                            for (int j = 0; j < 12; ++j) shv[j] = s4[j];
+                            for (int q = 0; q < 12; ++q) shv[q] = s4[q];
                         }
 #endif
                         if constexpr (PACK) {
@@ -715,8 +723,8 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                             const float l2 = len2(dk);
                             hacc = particle_alpha(ok, dk, l2, rec.density, a.min_response, a.alpha_min, halpha);
                         } else {
-                            halpha = ka[0];
-                            hacc = ka[0] > 0.0f;
+                            halpha = ka[j];
+                            hacc = ka[j] > 0.0f;
                         }
                         if (hacc) {
                             const float weight = halpha * T;
@@ -749,15 +757,17 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                             acc.w += 1.0f;
                             T *= (1.0f - halpha);
                         }
-                        last = fmaxf(last, kt[0]);
+                        last = fmaxf(last, kt[j]);
+                    }
+                    if (!__builtin_amdgcn_ballot_w64(go) || base + GVRT_COMP_UNROLL >= KB) break;
+#pragma unroll
+                    for (int i = 0; i < KB - GVRT_COMP_UNROLL; ++i) {
+                        kt[i] = kt[i + GVRT_COMP_UNROLL];
+                        kid[i] = kid[i + GVRT_COMP_UNROLL];
+                        if constexpr (!PACK) ka[i] = ka[i + GVRT_COMP_UNROLL];
                     }
 #pragma unroll
-                    for (int i = 0; i < KB - 1; ++i) {
-                        kt[i] = kt[i + 1];
-                        kid[i] = kid[i + 1];
-                        if constexpr (!PACK) ka[i] = ka[i + 1];
-                    }
-                    kid[KB - 1] = INVALID_ID;
+                    for (int i = KB - GVRT_COMP_UNROLL; i < KB; ++i) kid[i] = INVALID_ID;
                 }
                 active = (last <= s_tmax[wid][lane]) && (T > a.min_transmittance);
                 s_last[wid][lane] = last;
