@@ -58,6 +58,9 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 #ifndef GVRT_COMP_UNROLL
 #define GVRT_COMP_UNROLL 4
 #endif
+#ifndef GVRT_SKIP_EMPTY_ROUND
+#define GVRT_SKIP_EMPTY_ROUND 1
+#endif
 #ifndef GVRT_TCUT
 #define GVRT_TCUT 1
 #endif
@@ -690,6 +693,11 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                 float T = s_T[wid][lane];
                 float4 acc = s_acc[wid][lane];
                 float last = s_last[wid][lane];
+                // FAST: a buffer that did not fill holds every admitted crossing of (tlo, thi] (nothing was
+                // culled by kt[K-1]; what tcut culled lies past the slot where T drops below
+                // minTransmittance).  Once they are composited nothing is left, so the next round that
+                // the reference's loop would trace (and find empty) is skipped.
+                const bool full = LITERAL || !GVRT_SKIP_EMPTY_ROUND || kid[KB - 1] != INVALID_ID;
                 // Slots in groups of CU (static indices inside a group, so no per-hit register shift);
                 // the buffer shifts down by CU between groups.  Per lane: stop at the first empty slot
                 // or once T <= minTransmittance (slots are sorted with the empty ones last, T only falls).
@@ -769,7 +777,7 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
 #pragma unroll
                     for (int i = KB - GVRT_COMP_UNROLL; i < KB; ++i) kid[i] = INVALID_ID;
                 }
-                active = (last <= s_tmax[wid][lane]) && (T > a.min_transmittance);
+                active = full && (last <= s_tmax[wid][lane]) && (T > a.min_transmittance);
                 s_last[wid][lane] = last;
                 s_T[wid][lane] = T;
                 s_acc[wid][lane] = acc;
