@@ -19,14 +19,12 @@ namespace {
 
 constexpr uint32_t SPEC_DIM = 45;  // SPECULAR_DIMENSION, 3dgs.glsl:14
 
-// particlePrimitives.comp:120-140 — abnormal particle filter.  Reads f_rest of the next two
-// particles for i >= 15 (Q5); the buffer carries 90 zero floats past the end so the last two
-// particles read 0.0 there.
-__device__ inline bool survives(uint32_t g, const float* __restrict__ fdc, const float* __restrict__ frest) {
-    const float a0 = fdc[3 * g], a1 = fdc[3 * g + 1], a2 = fdc[3 * g + 2];
+// particlePrimitives.comp:120-140 — abnormal particle filter on one Gaussian's f_dc and the 45 f_rest
+// floats starting at its own (s[45..] are the next particles', Q5: the reference reads them for i >= 15;
+// the device buffer carries 90 zero floats past the end, so the last two particles read 0.0 there).
+__device__ inline bool survives(float a0, float a1, float a2, const float* s) {
     const float albedoStrength = sqrtf(a0 * a0 + a1 * a1 + a2 * a2);
     float specularStrength = 0.0f, maxSpecular = 0.0f, minSpecular = 1e10f;
-    const float* s = frest + (uint64_t)g * SPEC_DIM;
 #pragma unroll 4
     for (uint32_t i = 1; i < SPEC_DIM; i++) {
         const float x = s[3 * i], y = s[3 * i + 1], z = s[3 * i + 2];
@@ -39,12 +37,49 @@ __device__ inline bool survives(uint32_t g, const float* __restrict__ fdc, const
     return true;
 }
 
+// One block = 256 Gaussians.  The block's f_rest span (256 x 45 floats plus the 90 the Q5 neighbour reads
+// reach into) is staged in LDS with coalesced float4 loads; each thread then walks its own 45 floats
+// there (stride 45 words: odd, so the 64 lanes hit distinct banks).  Per-thread global reads at a 180-B
+// stride touched a different cache line in every lane of every load instruction.
+constexpr uint32_t FB = 256;                        // Gaussians per block
+constexpr uint32_t FSPAN = FB * SPEC_DIM + 2 * SPEC_DIM;  // staged floats (multiple of 4: 11610 -> pad)
+constexpr uint32_t FSPAN4 = (FSPAN + 3) / 4;
+
 __global__ __launch_bounds__(256) void k_enclose_flags(uint64_t n, const float* __restrict__ fdc,
                                                        const float* __restrict__ frest,
                                                        uint32_t* __restrict__ flags) {
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ float4 s_fr4[FSPAN4];
+    const uint64_t g0 = (uint64_t)blockIdx.x * FB;
+    // frest holds 45 n + 90 floats (zero tail) and g0 * 45 * 4 B is 16-B aligned (g0 is a multiple of 256)
+    const uint64_t avail = (n - g0) * SPEC_DIM + 2 * SPEC_DIM;  // floats readable from this block's start
+    const float4* src4 = reinterpret_cast<const float4*>(frest + g0 * SPEC_DIM);
+    float* s_fr = reinterpret_cast<float*>(s_fr4);
+    for (uint32_t i = threadIdx.x; i < FSPAN4; i += blockDim.x) {
+        if (4ull * i + 3 < avail) {
+            s_fr4[i] = src4[i];
+        } else {
+            for (uint32_t k = 0; k < 4; ++k) s_fr[4 * i + k] = 4ull * i + k < avail ? frest[g0 * SPEC_DIM + 4 * i + k] : 0.0f;
+        }
+    }
+    __syncthreads();
+    const uint64_t g = g0 + threadIdx.x;
     if (g >= n) return;
-    flags[g] = survives((uint32_t)g, fdc, frest) ? 1u : 0u;
+    const bool ok = survives(fdc[3 * g], fdc[3 * g + 1], fdc[3 * g + 2], s_fr + threadIdx.x * SPEC_DIM);
+    flags[g] = ok ? 1u : 0u;
+}
+
+// SH records [f_dc, f_rest] in compaction order (particlePrimitives.comp:207-214), one thread per
+// output float: consecutive threads write consecutive floats and read consecutive floats of one
+// Gaussian (the 48-float rows of consecutive survivors come from nearly consecutive sources).
+__global__ __launch_bounds__(256) void k_enclose_sh(const uint32_t* __restrict__ count, const uint32_t* __restrict__ src,
+                                                    const float* __restrict__ fdc, const float* __restrict__ frest,
+                                                    float* __restrict__ sh48) {
+    const uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= 48ull * *count) return;  // grid sized for n; the survivor count is scan[n]
+    const uint64_t sidx = o / 48;
+    const uint32_t c = (uint32_t)(o - 48 * sidx);
+    const uint64_t g = src[sidx];
+    sh48[o] = c < 3 ? fdc[3 * g + c] : frest[g * SPEC_DIM + (c - 3)];
 }
 
 __device__ __constant__ float c_icosa[12][3] = {
@@ -144,14 +179,7 @@ __global__ __launch_bounds__(256) void k_enclose_emit(EncloseArgs a) {
     dr[1] = make_float4(q[0], q[1], q[2], q[3]);
     dr[2] = make_float4(scl.x, scl.y, scl.z, 0.0f);
 
-    // SH record [f_dc, f_rest] (particlePrimitives.comp:207-214)
-    float* sr = a.sh48 + 48ull * saveIdx;
-    sr[0] = a.fdc[3 * g];
-    sr[1] = a.fdc[3 * g + 1];
-    sr[2] = a.fdc[3 * g + 2];
-    const float* fr = a.frest + 45ull * g;
-#pragma unroll 5
-    for (int i = 0; i < 45; ++i) sr[3 + i] = fr[i];
+    // (SH record: k_enclose_sh, coalesced, after this pass)
 
     // render record: what processHit derives per hit from the density record
     // (fetchParticleDensity + quaternionWXYZToMatrix, gaussianfunctions.glsl:89-101, utils.glsl:13-34)
@@ -252,6 +280,16 @@ gvrt_status gvrt_launch_enclose(gvrt_context* c, const gvrt_enclosing_params* p,
     if (e != hipSuccess) {
         gvrt_dfree(c, &tmp);
         return gvrt_hip_check(c, e, "k_enclose_emit");
+    }
+    {
+        const uint64_t nf = 48ull * n;
+        hipLaunchKernelGGL(k_enclose_sh, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, c->stream, c->d_scan + n,
+                           c->d_src, c->d_fdc, c->d_frest, c->d_sh48);
+        e = hipGetLastError();
+        if (e != hipSuccess) {
+            gvrt_dfree(c, &tmp);
+            return gvrt_hip_check(c, e, "k_enclose_sh");
+        }
     }
     GVRT_HIP(c, hipEventRecord(c->ev1, c->stream));
     uint32_t count = 0;
