@@ -399,32 +399,43 @@ __device__ inline float half_area(const float* b) {
     return ex * ey + ey * ez + ez * ex;
 }
 
-// Greedy surface-area collapse, one 4-wide level per launch (ctl = {begin, end, allocated, depth}):
-// a 4-wide node starts from its binary root's two children and opens the internal child with the
-// largest surface area until it holds four; its internal children become next-level 4-wide nodes
-// (ids allocated contiguously per level, so each level is one contiguous, breadth-first range).
+// Greedy surface-area collapse, one 4-wide level per launch: a 4-wide node starts from its binary
+// root's two children and opens the internal child with the largest surface area until it holds four;
+// its internal children become next-level 4-wide nodes.  Ids are allocated per level: level L holds
+// ids [base_L, base_L + cnt[L]) with base_L = cnt[0] + ... + cnt[L-1], and level L allocates its
+// children as base_{L+1} + atomicAdd(&cnt[L+1], 1) — every count a launch reads is final (its level
+// was filled by the previous launch), so no bookkeeping launch runs between levels.  The binary depth
+// of every slot rides along (bdep), giving the max leaf depth without a separate leaf-to-root walk.
+// ctl = {max 4-wide level, max binary leaf depth}.
 __global__ __launch_bounds__(256) void k_collapse_level(const BvhNode* __restrict__ bin, int32_t* __restrict__ src4,
+                                                        uint32_t* __restrict__ bdep, uint32_t* __restrict__ cnt,
                                                         uint32_t* __restrict__ ctl, uint32_t level,
                                                         Bvh4Node* __restrict__ out) {
-    const uint32_t begin = ctl[0], end = ctl[1];
+    uint32_t begin = 0;
+    for (uint32_t l = 0; l < level; ++l) begin += cnt[l];
+    const uint32_t end = begin + cnt[level];
     const uint64_t i = (uint64_t)begin + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= end) return;
-    const BvhNode n = bin[src4[i]];
+    // (no early return: the whole wave takes part in the id allocation below)
+    const bool live = i < end;
+    const BvhNode n = bin[live ? src4[i] : 0];
+    const uint32_t d0 = live ? bdep[i] : 0u;  // binary depth of this 4-wide node's binary root (root = 1)
     int32_t ref[BVH_W];
+    uint32_t rd[BVH_W];
     float box[BVH_W][6];
     const float* nb = reinterpret_cast<const float*>(&n);
     ref[0] = n.c0;
     ref[1] = n.c1;
+    rd[0] = rd[1] = d0 + 1;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
         box[0][k] = nb[k];
         box[1][k] = nb[6 + k];
     }
-    int cnt = 2;
-    while (cnt < BVH_W) {
+    int cnt_s = 2;
+    while (live && cnt_s < BVH_W) {
         int best = -1;
         float ba = -1.0f;
-        for (int j = 0; j < cnt; ++j) {
+        for (int j = 0; j < cnt_s; ++j) {
             if (ref[j] >= 0) {
                 const float ar = half_area(box[j]);
                 if (ar > ba) {
@@ -436,45 +447,67 @@ __global__ __launch_bounds__(256) void k_collapse_level(const BvhNode* __restric
         if (best < 0) break;
         const BvhNode g = bin[ref[best]];
         const float* gb = reinterpret_cast<const float*>(&g);
-        for (int j = cnt; j > best + 1; --j) {  // keep the children in order (c0 before c1)
+        const uint32_t gd = rd[best] + 1;
+        for (int j = cnt_s; j > best + 1; --j) {  // keep the children in order (c0 before c1)
             ref[j] = ref[j - 1];
+            rd[j] = rd[j - 1];
             for (int k = 0; k < 6; ++k) box[j][k] = box[j - 1][k];
         }
         ref[best] = g.c0;
         ref[best + 1] = g.c1;
+        rd[best] = rd[best + 1] = gd;
         for (int k = 0; k < 6; ++k) {
             box[best][k] = gb[k];
             box[best + 1][k] = gb[6 + k];
         }
-        ++cnt;
+        ++cnt_s;
     }
+    // next-level ids: one atomic per wave (a single counter per level took one atomic per node, all on
+    // one address), lanes offset by an exclusive prefix sum of their internal-child counts
+    uint32_t nin = 0;
+    if (live)
+        for (int j = 0; j < cnt_s; ++j) nin += ref[j] >= 0 ? 1u : 0u;
+    const int lane = (int)(threadIdx.x & 63);
+    uint32_t incl = nin;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)incl, off, 64);
+        if (lane >= off) incl += v;
+    }
+    const uint32_t wtotal = (uint32_t)__shfl((int)incl, 63, 64);
+    uint32_t wbase = 0;
+    if (lane == 0 && wtotal) wbase = atomicAdd(cnt + level + 1, wtotal);
+    wbase = (uint32_t)__shfl((int)wbase, 0, 64);
+    // the wave's deepest binary leaf and whether it made any next-level node: one atomic each per wave
+    uint32_t ld = 0;
+    if (live)
+        for (int j = 0; j < cnt_s; ++j) ld = ref[j] < 0 ? max(ld, rd[j]) : ld;
+    for (int off = 32; off > 0; off >>= 1) ld = max(ld, (uint32_t)__shfl_xor((int)ld, off, 64));
+    if (lane == 0) {
+        if (wtotal) atomicMax(ctl + 0, level + 1);
+        if (ld) atomicMax(ctl + 1, ld);
+    }
+    if (!live) return;
+    uint32_t next_id = end + wbase + (incl - nin);  // level + 1 starts right after this level
     Bvh4Node o;
-    bool inner = false;
     uint32_t imask = 0;
-    for (int j = 0; j < cnt; ++j) {
+    for (int j = 0; j < cnt_s; ++j) {
         int32_t r = ref[j];
         if (r >= 0) {
-            const uint32_t id = atomicAdd(ctl + 2, 1u);
+            const uint32_t id = next_id++;
             src4[id] = r;
+            bdep[id] = rd[j];
             r = (int32_t)id;
-            inner = true;
             imask |= 1u << j;
         }
         put_slot(o, j, box[j], r);
     }
     const float eb[6] = {EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX};
-    o.nchild = (uint32_t)cnt;
-    for (int j = cnt; j < BVH_W; ++j) put_slot(o, j, eb, 0);
+    o.nchild = (uint32_t)cnt_s;
+    for (int j = cnt_s; j < BVH_W; ++j) put_slot(o, j, eb, 0);
     o.pad[0] = n.pad0;  // split axis of the binary root (children are in its in-order)
     o.pad[1] = imask;   // children that are 4-wide nodes
     o.pad[2] = 0;
     out[i] = o;
-    if (inner) atomicMax(ctl + 3, level + 1);
-}
-
-__global__ void k_level_advance(uint32_t* ctl) {
-    ctl[0] = ctl[1];
-    ctl[1] = ctl[2];
 }
 
 }  // namespace
@@ -627,7 +660,7 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
     std::vector<const float*> hlv(nlev, nullptr);
     if (nlev > 1) TRY(gvrt_dalloc(c, (void**)&stab, 24ull * m * (nlev - 1)));
     TRY(gvrt_dalloc(c, (void**)&dlv, sizeof(float*) * nlev));
-    TRY(gvrt_dalloc(c, (void**)&dep, 32));
+    TRY(gvrt_dalloc(c, (void**)&dep, 4 * (8 + 128)));  // collapse control + per-level counts
     TRY(gvrt_dalloc(c, (void**)&lpar, 4ull * m));
     TRY(gvrt_dalloc(c, (void**)&npar, 4ull * ninternal));
     TRY(gvrt_dalloc(c, (void**)&lboxes, 24ull * m));
@@ -700,39 +733,58 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
             hipLaunchKernelGGL(k_karras, dim3(iblocks), dim3(256), 0, c->stream, m, keys2, c->d_nodes, lpar, npar,
                                (const float* const*)dlv);
         }
-        hipLaunchKernelGGL(k_depth, dim3(blocks), dim3(256), 0, c->stream, m, lpar, npar, dep);
-        TRYH(hipGetLastError(), "k_karras");
-        uint32_t hd = 0;
-        TRYH(hipMemcpyAsync(&hd, dep, 4, hipMemcpyDeviceToHost, c->stream), "depth");
         const int64_t ni = m - 1;
         const char* ce = getenv("GVRT_COLLAPSE");
         // the even-depth rule needs the Karras layout and 4-wide nodes
         const bool greedy = ploc || BVH_W != 4 || !(ce && ce[0] == '0');
+        TRYH(hipGetLastError(), "k_karras");
         if (greedy) {
             // ---- greedy surface-area collapse, level by level (upper bound: one 4-wide node per binary node)
-            int32_t* src4 = lpar;  // lpar (m entries) is free after k_depth
-            uint32_t* ctl = dep + 4;  // dep: [0] depth census, [4..7] collapse control
-            const uint32_t ctl0[4] = {0u, 1u, 1u, 0u};
-            TRYH(hipMemcpyAsync(ctl, ctl0, 16, hipMemcpyHostToDevice, c->stream), "ctl");
+            int32_t* src4 = lpar;                                  // lpar (m entries) is free after the hierarchy
+            uint32_t* bdep = reinterpret_cast<uint32_t*>(keys);    // the sort keys are free too (8m bytes)
+            uint32_t* cnt = dep + 8;                               // per-level counts (MAX_LEVELS)
+            uint32_t* ctl = dep;                                   // {max 4-wide level, max binary leaf depth}
+            constexpr uint32_t MAX_LEVELS = 120;
+            TRYH(hipMemsetAsync(dep, 0, 4 * (8 + MAX_LEVELS + 1), c->stream), "ctl");
+            const uint32_t one = 1u;
+            TRYH(hipMemcpyAsync(cnt, &one, 4, hipMemcpyHostToDevice, c->stream), "cnt0");
             TRYH(hipMemcpyAsync(src4, &root, 4, hipMemcpyHostToDevice, c->stream), "src4");
-            TRYH(hipStreamSynchronize(c->stream), "sync");  // hd (binary depth) bounds the level count
+            TRYH(hipMemcpyAsync(bdep, &one, 4, hipMemcpyHostToDevice, c->stream), "bdep");
+            // launches in chunks of 8 levels; after each chunk the count of the next level says whether
+            // the tree goes deeper (one small readback per chunk instead of a depth census)
             uint64_t width = 1;
-            for (uint32_t lv = 0; lv <= hd; ++lv) {
-                const uint64_t w = width < (uint64_t)ni ? width : (uint64_t)ni;
-                hipLaunchKernelGGL(k_collapse_level, dim3((unsigned)((w + 255) / 256)), dim3(256), 0, c->stream, c->d_nodes,
-                                   src4, ctl, lv, c->d_nodes4);
-                hipLaunchKernelGGL(k_level_advance, dim3(1), dim3(1), 0, c->stream, ctl);
-                width = width * BVH_W < (uint64_t)ni ? width * BVH_W : (uint64_t)ni;
+            uint32_t lv = 0;
+            while (lv < MAX_LEVELS) {
+                const uint32_t stop = std::min(lv + 8, MAX_LEVELS);
+                for (; lv < stop; ++lv) {
+                    const uint64_t w = width < (uint64_t)ni ? width : (uint64_t)ni;
+                    hipLaunchKernelGGL(k_collapse_level, dim3((unsigned)((w + 255) / 256)), dim3(256), 0, c->stream,
+                                       c->d_nodes, src4, bdep, cnt, ctl, lv, c->d_nodes4);
+                    width = width * BVH_W < (uint64_t)ni ? width * BVH_W : (uint64_t)ni;
+                }
+                uint32_t pending = 0;
+                TRYH(hipMemcpyAsync(&pending, cnt + lv, 4, hipMemcpyDeviceToHost, c->stream), "cnt");
+                TRYH(hipStreamSynchronize(c->stream), "sync");
+                if (pending == 0) break;
             }
             TRYH(hipGetLastError(), "k_collapse_level");
-            uint32_t hc[4];
-            TRYH(hipMemcpyAsync(hc, ctl, 16, hipMemcpyDeviceToHost, c->stream), "ctl");
+            if (lv >= MAX_LEVELS) TRY(gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "4-wide collapse deeper than 120 levels"));
+            uint32_t hc[2];
+            std::vector<uint32_t> hcnt(MAX_LEVELS);
+            TRYH(hipMemcpyAsync(hc, ctl, 8, hipMemcpyDeviceToHost, c->stream), "ctl");
+            TRYH(hipMemcpyAsync(hcnt.data(), cnt, 4 * MAX_LEVELS, hipMemcpyDeviceToHost, c->stream), "cnt");
             TRYH(hipStreamSynchronize(c->stream), "sync");
-            c->depth = hd;
-            c->depth4 = hc[3] + 1;
-            c->n_nodes4 = hc[2];
+            uint32_t total = 0;
+            for (uint32_t v : hcnt) total += v;
+            c->depth = hc[1];
+            c->depth4 = hc[0] + 1;
+            c->n_nodes4 = total;
         } else {
         // ---- collapse to the 4-wide tree by even depth (reuse keys/vals as flags / scan)
+        TRYH(hipMemsetAsync(dep, 0, 4, c->stream), "memset");
+        hipLaunchKernelGGL(k_depth, dim3(blocks), dim3(256), 0, c->stream, m, lpar, npar, dep);
+        uint32_t hd = 0;
+        TRYH(hipMemcpyAsync(&hd, dep, 4, hipMemcpyDeviceToHost, c->stream), "depth");
         uint32_t* flags = reinterpret_cast<uint32_t*>(keys);
         hipLaunchKernelGGL(k_even_flags, dim3((unsigned)((ni + 1 + 255) / 256)), dim3(256), 0, c->stream, ni, npar,
                            flags);
