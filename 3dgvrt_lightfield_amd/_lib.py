@@ -60,7 +60,8 @@ class Image(C.Structure):
 
 
 class AccelParams(C.Structure):
-    _fields_ = [("split_cells", C.c_uint32), ("builder", C.c_uint32), ("reserved", C.c_uint32 * 6)]
+    _fields_ = [("split_cells", C.c_uint32), ("builder", C.c_uint32), ("collapse", C.c_uint32),
+                ("reserved", C.c_uint32 * 5)]
 
 
 class Stats(C.Structure):

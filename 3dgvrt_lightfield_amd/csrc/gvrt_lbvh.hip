@@ -14,6 +14,8 @@
 //   7. depth census           (guards the render kernel's fixed LDS stack)
 #include <hipcub/hipcub.hpp>
 
+#include <cstring>
+#include <functional>
 #include <vector>
 
 #include "gvrt_internal.h"
@@ -512,6 +514,137 @@ __global__ __launch_bounds__(256) void k_collapse_level(const BvhNode* __restric
 
 }  // namespace
 
+// Surface-area-optimal 4-wide collapse (dynamic programming over the binary tree, after Ylitie, Karras
+// and Laine, "Efficient Incoherent Ray Traversal on GPUs Through Compressed Wide BVHs", HPG 2017 §4),
+// host-side experiment (GVRT_COLLAPSE=dp).  With one proxy per leaf the leaf term of the SAH is the same
+// for every collapse, so the DP minimises the summed surface area of the 4-wide nodes:
+//   F(leaf, k) = 0;  F(n, 1) = C(n) = SA(n) + min_j F(c0, j) + F(c1, 4 - j);
+//   F(n, k) = min(F(n, k - 1), min_j F(c0, j) + F(c1, k - j))   (k = 2..4)
+// and the tree is rebuilt top-down, breadth-first, children in the binary in-order (split-axis order).
+static float host_area(const float* b) {
+    const float ex = b[3] - b[0], ey = b[4] - b[1], ez = b[5] - b[2];
+    return ex * ey + ey * ez + ez * ex;
+}
+
+static gvrt_status host_dp_collapse(gvrt_context* c, int32_t root, uint64_t m, uint32_t* depth_out,
+                                    uint32_t* depth4_out, uint64_t* n4_out) {
+    const uint64_t ni = m - 1;
+    std::vector<BvhNode> bn(ni);
+    GVRT_HIP(c, hipMemcpyAsync(bn.data(), c->d_nodes, sizeof(BvhNode) * ni, hipMemcpyDeviceToHost, c->stream));
+    GVRT_HIP(c, hipStreamSynchronize(c->stream));
+    // F[n][k-1], k = 1..4, bottom-up by an explicit post-order walk
+    std::vector<float> F(4 * ni, 0.0f);
+    auto f = [&](int32_t x, int k) -> float { return x < 0 ? 0.0f : F[4 * (uint64_t)x + (k - 1)]; };
+    std::vector<std::pair<int32_t, uint32_t>> st;  // (node, binary depth)
+    std::vector<uint8_t> seen(ni, 0);
+    uint32_t maxd = 0;
+    st.push_back({root, 1});
+    while (!st.empty()) {
+        const auto [x, dx] = st.back();
+        const BvhNode& n = bn[x];
+        if (!seen[x]) {
+            seen[x] = 1;
+            if (n.c0 >= 0) st.push_back({n.c0, dx + 1}); else maxd = std::max(maxd, dx + 1);
+            if (n.c1 >= 0) st.push_back({n.c1, dx + 1}); else maxd = std::max(maxd, dx + 1);
+            continue;
+        }
+        st.pop_back();
+        const float* nb = reinterpret_cast<const float*>(&n);
+        float ub[6];
+        for (int k = 0; k < 3; ++k) {
+            ub[k] = std::min(nb[k], nb[6 + k]);
+            ub[3 + k] = std::max(nb[3 + k], nb[9 + k]);
+        }
+        float best4 = INFINITY;
+        for (int j = 1; j < 4; ++j) best4 = std::min(best4, f(n.c0, j) + f(n.c1, 4 - j));
+        float* Fx = &F[4 * (uint64_t)x];
+        Fx[0] = host_area(ub) + best4;
+        for (int k = 2; k <= 4; ++k) {
+            float b = Fx[k - 2];
+            for (int j = 1; j < k; ++j) b = std::min(b, f(n.c0, j) + f(n.c1, k - j));
+            Fx[k - 1] = b;
+        }
+    }
+    // frontier of node x (box bx) in at most k pieces
+    struct Piece { int32_t ref; float box[6]; };
+    std::function<void(int32_t, const float*, int, std::vector<Piece>&)> expand =
+        [&](int32_t x, const float* bx, int k, std::vector<Piece>& out) {
+            if (x < 0 || k == 1) {
+                Piece p;
+                p.ref = x;
+                std::memcpy(p.box, bx, 24);
+                out.push_back(p);
+                return;
+            }
+            if (F[4 * (uint64_t)x + (k - 1)] == F[4 * (uint64_t)x + (k - 2)]) {
+                expand(x, bx, k - 1, out);
+                return;
+            }
+            const BvhNode& n = bn[x];
+            const float* nb = reinterpret_cast<const float*>(&n);
+            int bj = 1;
+            float bv = INFINITY;
+            for (int j = 1; j < k; ++j) {
+                const float v = f(n.c0, j) + f(n.c1, k - j);
+                if (v < bv) bv = v, bj = j;
+            }
+            expand(n.c0, nb, bj, out);
+            expand(n.c1, nb + 6, k - bj, out);
+        };
+    std::vector<Bvh4Node> outn;
+    outn.reserve(ni);
+    std::vector<int32_t> queue{root};
+    std::vector<uint32_t> qlev{0};
+    uint32_t maxlev = 0;
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+        const int32_t x = queue[qi];
+        const BvhNode& n = bn[x];
+        const float* nb = reinterpret_cast<const float*>(&n);
+        int bj = 1;
+        float bv = INFINITY;
+        for (int j = 1; j < 4; ++j) {
+            const float v = f(n.c0, j) + f(n.c1, 4 - j);
+            if (v < bv) bv = v, bj = j;
+        }
+        std::vector<Piece> ps;
+        expand(n.c0, nb, bj, ps);
+        expand(n.c1, nb + 6, 4 - bj, ps);
+        Bvh4Node o{};
+        uint32_t imask = 0;
+        for (size_t j = 0; j < ps.size(); ++j) {
+            int32_t r = ps[j].ref;
+            if (r >= 0) {
+                r = (int32_t)queue.size();
+                queue.push_back(ps[j].ref);
+                qlev.push_back(qlev[qi] + 1);
+                maxlev = std::max(maxlev, qlev[qi] + 1);
+                imask |= 1u << j;
+            }
+            const float* b = ps[j].box;
+            o.box[j][0] = b[0]; o.box[j][1] = b[3];
+            o.box[j][2] = b[1]; o.box[j][3] = b[4];
+            o.box[j][4] = b[2]; o.box[j][5] = b[5];
+            o.child[j] = r;
+        }
+        for (size_t j = ps.size(); j < (size_t)BVH_W; ++j) {
+            for (int k = 0; k < 6; ++k) o.box[j][k] = EMPTY_BOX;
+            o.child[j] = 0;
+        }
+        o.nchild = (uint32_t)ps.size();
+        o.pad[0] = n.pad0;
+        o.pad[1] = imask;
+        o.pad[2] = 0;
+        outn.push_back(o);
+    }
+    GVRT_HIP(c, hipMemcpyAsync(c->d_nodes4, outn.data(), sizeof(Bvh4Node) * outn.size(), hipMemcpyHostToDevice,
+                               c->stream));
+    GVRT_HIP(c, hipStreamSynchronize(c->stream));
+    *depth_out = maxd;
+    *depth4_out = maxlev + 1;
+    *n4_out = outn.size();
+    return GVRT_OK;
+}
+
 gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap) {
     const int64_t mp = (int64_t)c->m;  // proxies (survivors)
     gvrt_dfree(c, (void**)&c->d_recs);
@@ -738,7 +871,14 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
         // the even-depth rule needs the Karras layout and 4-wide nodes
         const bool greedy = ploc || BVH_W != 4 || !(ce && ce[0] == '0');
         TRYH(hipGetLastError(), "k_karras");
-        if (greedy) {
+        if ((ap.collapse == 1 || (ce && ce[0] == 'd')) && BVH_W == 4) {
+            uint32_t d2 = 0, d4 = 0;
+            uint64_t n4 = 0;
+            TRY(host_dp_collapse(c, root, m, &d2, &d4, &n4));
+            c->depth = d2;
+            c->depth4 = d4;
+            c->n_nodes4 = n4;
+        } else if (greedy) {
             // ---- greedy surface-area collapse, level by level (upper bound: one 4-wide node per binary node)
             int32_t* src4 = lpar;                                  // lpar (m entries) is free after the hierarchy
             uint32_t* bdep = reinterpret_cast<uint32_t*>(keys);    // the sort keys are free too (8m bytes)

@@ -122,17 +122,17 @@ class Renderer:
             out["verts"], out["tris"] = verts, tris
         return out
 
-    def build_accel(self, split_cells=0, builder=0):
+    def build_accel(self, split_cells=0, builder=0, collapse=0):
         p = _lib.AccelParams()
         lib().gvrt_default_accel_params(C.byref(p))
-        p.split_cells, p.builder = int(split_cells), int(builder)
+        p.split_cells, p.builder, p.collapse = int(split_cells), int(builder), int(collapse)
         check(lib().gvrt_build_accel_ex(self.h, C.byref(p)), self.h)
 
-    def prepare(self, splats, split_cells=0, builder=0, **enclosing):
+    def prepare(self, splats, split_cells=0, builder=0, collapse=0, **enclosing):
         """VulkanFullRT::prepare: upload, enclose, build the acceleration structure."""
         self.load_splats(splats)
         m = self.build_enclosing(**enclosing)
-        self.build_accel(split_cells=split_cells, builder=builder)
+        self.build_accel(split_cells=split_cells, builder=builder, collapse=collapse)
         return m
 
     def set_stats(self, on=True):

@@ -103,3 +103,32 @@ def test_split_tiny_scenes_and_limits(gv, O):
             r.build_accel(split_cells=1024)
         with pytest.raises(gv.GvrtError):
             r.build_accel(builder=2)
+
+
+@pytest.mark.parametrize("split", [0, 10])
+def test_sah_optimal_collapse_same_image(gv, O, config1, config1_enc, split):
+    """gvrt_accel_params.collapse = 1 (surface-area-optimal 4-wide collapse) changes only the tree: the
+    image and the literal crossing counts are those of the greedy collapse (same tolerances as above)."""
+    W = H = 160
+    vi, pi = gv.scene.config1_camera(W, H)
+    with gv.Renderer(0) as r:
+        r.prepare(config1, split_cells=split)
+        base = {mode: r.render(vi, pi, W, H, mode=mode, hit_counts=True) for mode in (0, 1)}
+        nodes0 = r.stats()["bvh_nodes"]
+        r.set_stats(True)
+        r.render(vi, pi, W, H, mode=gv.MODE_LITERAL)
+        st0 = r.stats()
+        r.build_accel(split_cells=split, collapse=1)
+        st = r.stats()
+        assert st["bvh_nodes"] > 0 and st["bvh_depth"] == st0["bvh_depth"]
+        r.render(vi, pi, W, H, mode=gv.MODE_LITERAL)
+        st1 = r.stats()
+        r.set_stats(False)
+        for mode in (0, 1):
+            out = r.render(vi, pi, W, H, mode=mode, hit_counts=True)
+            _close(out["rgba32f"], base[mode]["rgba32f"])
+        with pytest.raises(RuntimeError):
+            r.build_accel(collapse=2)
+    for k in ("crossings", "accepted"):
+        assert abs(int(st1[k]) - int(st0[k])) <= 1e-4 * st0[k] + 2, (k, st1[k], st0[k])
+    assert nodes0 > 0
