@@ -302,7 +302,13 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
     a.nrecs = (uint32_t)c->m;
     // cameras
     if ((s = ensure(c, (void**)&c->d_viewinv, &c->viewinv_cap, 64ull * ncams))) return s;
-    GVRT_HIP(c, hipMemcpyAsync(c->d_viewinv, view_inverse, 64ull * ncams, hipMemcpyHostToDevice, c->stream));
+    // the camera matrices go up only when they changed (a pageable 64-B upload costs a host round trip
+    // per frame for a static camera)
+    if (c->h_viewinv.size() != 16ull * ncams ||
+        std::memcmp(c->h_viewinv.data(), view_inverse, 64ull * ncams) != 0) {
+        c->h_viewinv.assign(view_inverse, view_inverse + 16ull * ncams);
+        GVRT_HIP(c, hipMemcpyAsync(c->d_viewinv, c->h_viewinv.data(), 64ull * ncams, hipMemcpyHostToDevice, c->stream));
+    }
     a.view_inv = c->d_viewinv;
     std::memcpy(a.proj_inv, proj_inverse, 64);
     std::memcpy(a.aabb, p->aabb, 24);

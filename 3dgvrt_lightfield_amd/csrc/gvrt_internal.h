@@ -4,6 +4,7 @@
 
 #include <string>
 #include <unordered_map>
+#include <vector>
 
 #include "../../include/gvrt.h"
 #include "gvrt_device.h"
@@ -64,6 +65,7 @@ struct gvrt_context {
     uint64_t tiles_cap = 0;
     float* d_viewinv = nullptr;
     uint64_t viewinv_cap = 0;
+    std::vector<float> h_viewinv;  // host copy of what d_viewinv holds
     void* d_stage = nullptr;  // staging for host outputs
     uint64_t stage_cap = 0;
 

@@ -58,6 +58,7 @@ class Renderer:
         self.h = h
         self.device = device
         self.m = 0
+        self._ms_stats = _lib.Stats()
 
     def close(self):
         if self.h:
@@ -144,6 +145,12 @@ class Renderer:
         out = {k: getattr(s, k) for k, _ in s._fields_ if not k.startswith("pad")}
         out["phase_cycles"] = list(out["phase_cycles"])
         return out
+
+    def render_ms(self):
+        """Device time of the last render kernel (gvrt_stats.render_ms) without building the stats dict."""
+        s = self._ms_stats
+        check(lib().gvrt_get_stats(self.h, C.byref(s)), self.h)
+        return s.render_ms
 
     @staticmethod
     def tile_array(tiles):

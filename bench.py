@@ -140,7 +140,7 @@ def main():
         finish(b)
         r.render_device(vi, pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=frames[b].data_ptr(),
                         packed=args.split == "tiles")
-        kernel_ms.append(r.stats()["render_ms"])
+        kernel_ms.append(r.render_ms())
         if distributed:
             if args.split == "views":
                 pending[b] = dist.gather(frames[b], gathered[b] if rank == 0 else None, dst=0, async_op=True)
