@@ -98,6 +98,28 @@ def test_fast_equals_literal(renderer, gv, config1):
     assert (fa[:, 3] != fb[:, 3]).mean() <= 2e-4
 
 
+def test_fast_skips_the_empty_trailing_round(renderer, gv, config1):
+    """A FAST k-buffer that did not fill held every admitted crossing, so the round the reference would
+    trace next (and find empty) is skipped: on the sparse config-1 scene most rays leave it unterminated,
+    and each of them costs LITERAL (the reference's loop) one more, empty round than FAST; the images
+    agree as in test_fast_equals_literal."""
+    renderer.prepare(config1)
+    W = H = 96
+    vi, pi = gv.scene.config1_camera(W, H)
+    renderer.set_stats(True)
+    try:
+        fast = renderer.render(vi, pi, W, H, mode=gv.MODE_FAST, kbuffer_depth=32)
+        sf = renderer.stats()
+        lit = renderer.render(vi, pi, W, H, mode=gv.MODE_LITERAL)
+        sl = renderer.stats()
+    finally:
+        renderer.set_stats(False)
+    assert sf["rounds"] < sl["rounds"], (sf["rounds"], sl["rounds"])
+    fa, fb = fast["rgba32f"].reshape(-1, 4), lit["rgba32f"].reshape(-1, 4)
+    d = np.abs(fa[:, :3] - fb[:, :3]).max(axis=1)
+    assert (d > 1e-4).mean() <= 2e-4 and d.max() <= 0.05
+
+
 def test_literal_stats_match_oracle(renderer, gv, O, config1, config1_enc):
     renderer.prepare(config1)
     renderer.set_stats(True)
@@ -200,6 +222,24 @@ def test_deterministic_repeat(renderer, gv, config1):
     renderer.prepare(config1)  # rebuild everything
     b = renderer.render(vi, pi, 128, 128)["rgba32f"]
     np.testing.assert_array_equal(a, b)
+
+
+def test_camera_change_between_renders(renderer, gv, config1):
+    """The handle re-uploads the camera matrices only when they change: alternating two cameras on one
+    handle gives each camera's own image, equal to a fresh handle's."""
+    renderer.prepare(config1)
+    W = H = 64
+    via, pi = gv.scene.config1_camera(W, H)
+    vib = np.array(via, np.float32).reshape(4, 4).copy()
+    vib[3, :3] += np.float32(0.25)  # column-major: translation in elements 12..14
+    a1 = renderer.render(via, pi, W, H)["rgba32f"]
+    b1 = renderer.render(vib.reshape(-1), pi, W, H)["rgba32f"]
+    a2 = renderer.render(via, pi, W, H)["rgba32f"]
+    assert not np.array_equal(a1, b1)
+    np.testing.assert_array_equal(a1, a2)
+    with gv.Renderer(0) as r2:
+        r2.prepare(config1)
+        np.testing.assert_array_equal(r2.render(vib.reshape(-1), pi, W, H)["rgba32f"], b1)
 
 
 # ------------------------------------------------------------------ full-size (bench scene) properties
