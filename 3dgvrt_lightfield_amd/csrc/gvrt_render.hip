@@ -362,12 +362,23 @@ __device__ inline float unif(float v) { return __int_as_float(__builtin_amdgcn_r
 
 // Waves per SIMD the register allocator must fit: 4 (<= 128 VGPRs) measured fastest, ahead of 3 (no
 // spills) and 5 (heavy spills); see DESIGN.md §4.
+// Workgroup shape: GVRT_WG_WAVES waves (8x8 tiles) per workgroup, laid out GVRT_WG_TW tiles wide.
+// 2 x 2 tiles (16 x 16 px) measured ~1 % ahead of 4 x 1; 8-wave workgroups (8 x 1, 4 x 2) 13 % behind.
+#ifndef GVRT_WG_WAVES
+#define GVRT_WG_WAVES 4
+#endif
+#ifndef GVRT_WG_TW
+#define GVRT_WG_TW 2
+#endif
+constexpr int WGW = GVRT_WG_WAVES, WG_TW = GVRT_WG_TW, WG_TH = GVRT_WG_WAVES / GVRT_WG_TW;
+static_assert(WG_TW * WG_TH == WGW, "workgroup tile block");
+
 #ifndef GVRT_RENDER_MIN_WAVES
 #define GVRT_RENDER_MIN_WAVES 4
 #endif
 
 template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK>
-__global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const RenderArgs a, const Bvh4Node* __restrict__ nodes_,
+__global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_render(const RenderArgs a, const Bvh4Node* __restrict__ nodes_,
                                                 const RenderRec* __restrict__ recs_, const RenderRec* __restrict__ crecs_,
                                                 const uint4* __restrict__ aux_, const float* __restrict__ sh_,
                                                 const float* __restrict__ view_inv_, const uint32_t* __restrict__ tiles_,
@@ -376,34 +387,37 @@ __global__ __launch_bounds__(256, GVRT_RENDER_MIN_WAVES) void k_render(const Ren
                                                 unsigned long long* __restrict__ stats_) {
     // SH basis of each lane's ray direction, chunk-major so one ds_read_b128 per chunk is
     // conflict-free (16 KB per block; occupancy is VGPR-bound, not LDS-bound)
-    __shared__ float4 s_basis[4][4][64];
+    __shared__ float4 s_basis[WGW][4][64];
     // composite state (rgb, alpha accumulator) and transmittance, parked in LDS during traversal so
     // their VGPRs go to the k-buffer (2 x KB registers)
-    __shared__ float4 s_acc[4][64];
-    __shared__ float s_T[4][64];
-    __shared__ float s_last[4][64];  // `last` and the AABB exit: round-boundary state, not needed in traversal
-    __shared__ float s_tmax[4][64];
+    __shared__ float4 s_acc[WGW][64];
+    __shared__ float s_T[WGW][64];
+    __shared__ float s_last[WGW][64];  // `last` and the AABB exit: round-boundary state, not needed in traversal
+    __shared__ float s_tmax[WGW][64];
 #if !GVRT_VSTACK
-    __shared__ int32_t s_stack[4][STACK_DEPTH];
+    __shared__ int32_t s_stack[WGW][STACK_DEPTH];
 #endif
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     // (Round-robin workgroup -> XCD dealing is kept: an XCD-contiguous band remap measured 33 % slower,
     // the bands' very different costs leave a long tail; L2 hit rate is already ~91 %.)
-    const uint64_t tile_idx = (uint64_t)blockIdx.x * 4 + wid;
-    if (tile_idx >= a.ntiles) return;  // wave-uniform
+    const uint64_t tile_idx = (uint64_t)blockIdx.x * WGW + wid;  // tile-list position
     uint32_t cam, tx, ty;
     if (tiles_) {
+        if (tile_idx >= a.ntiles) return;  // wave-uniform
         const uint32_t t = tiles_[tile_idx];
         cam = t >> 24;
         ty = (t >> 12) & 0xFFFu;
         tx = t & 0xFFFu;
     } else {
-        const uint64_t per = (uint64_t)a.tiles_x * a.tiles_y;
-        cam = (uint32_t)(tile_idx / per);
-        const uint32_t rem = (uint32_t)(tile_idx % per);
-        ty = rem / a.tiles_x;
-        tx = rem % a.tiles_x;
+        // workgroup = a WG_TW x WG_TH block of tiles, blocks row-major per camera
+        const uint32_t bx_n = (a.tiles_x + WG_TW - 1) / WG_TW, by_n = (a.tiles_y + WG_TH - 1) / WG_TH;
+        const uint64_t per = (uint64_t)bx_n * by_n;
+        cam = (uint32_t)(blockIdx.x / per);
+        const uint32_t rem = (uint32_t)(blockIdx.x % per);
+        ty = (rem / bx_n) * WG_TH + (uint32_t)wid / WG_TW;
+        tx = (rem % bx_n) * WG_TW + (uint32_t)wid % WG_TW;
+        if (tx >= a.tiles_x || ty >= a.tiles_y) return;  // wave-uniform: tile outside the frame
     }
     cam = uni(cam);
     const uint32_t px = tx * 8 + (lane & 7), py = ty * 8 + (lane >> 3);
@@ -852,11 +866,13 @@ __global__ __launch_bounds__(256) void k_unpack(const uint32_t* __restrict__ pac
 }  // namespace
 
 gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64_t nwaves, bool literal) {
-    const uint64_t blocks = (nwaves + 3) / 4;
-    if (blocks == 0) return GVRT_OK;
+    uint64_t blocks = (nwaves + WGW - 1) / WGW;
+    if (!a.tiles)
+        blocks = (uint64_t)((a.tiles_x + WG_TW - 1) / WG_TW) * ((a.tiles_y + WG_TH - 1) / WG_TH) * a.ncams;
+    if (nwaves == 0 || blocks == 0) return GVRT_OK;
     if (blocks > 0x7FFFFFFFull) return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "too many tiles");
     const bool adaptive = (a.kopts & 1u) != 0;
-    const dim3 g((unsigned)blocks), b(256);
+    const dim3 g((unsigned)blocks), b(64 * WGW);
     // every pointer is its own __restrict__ argument: the uniform node / record loads can then be
     // proven unclobbered by the output stores and are emitted as scalar (s_load) loads
 #define KARGS a.nodes, a.recs, a.crecs, a.aux, a.sh, a.view_inv, a.tiles, a.rgba8, a.rgba32f, a.ray_dirs, a.hit_counts, a.stats
