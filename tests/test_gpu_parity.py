@@ -224,6 +224,33 @@ def test_deterministic_repeat(renderer, gv, config1):
     np.testing.assert_array_equal(a, b)
 
 
+# Non-default UBO parameters (UniformDataStatic, base/VulkanUtils.h:50-68): the
+# HIP path and the oracle take the same values.  The scene AABB box of ±0.6 around the cloud clips rays
+# (Q12: /max(dir, 1e-6) leaves negative direction components unconstrained); the iteration cap is the
+# reference's ITERATIONS debug switch (raygen.rgen:140-143), LITERAL mode only.
+@pytest.mark.parametrize("mode,kw", [
+    (0, {"sph_eval_degree": 0}),
+    (0, {"sph_eval_degree": 1}),
+    (1, {"sph_eval_degree": 2}),
+    (0, {"aabb": (-0.6, -0.6, -0.6, 0.6, 0.6, 0.6)}),
+    (1, {"aabb": (-0.3, -1.0, -0.8, 0.9, 0.4, 1.0)}),
+    (0, {"min_transmittance": 0.05}),
+    (1, {"min_transmittance": 0.2}),
+    (0, {"hit_min_gaussian_response": 0.2}),
+    (0, {"alpha_min": 0.05}),
+    (1, {"max_rounds": 1}),
+    (1, {"max_rounds": 2, "kbuffer_depth": 0}),
+])
+def test_render_params_vs_oracle(renderer, gv, O, config1, config1_enc, mode, kw):
+    renderer.prepare(config1)
+    W = H = 96
+    vi, pi = gv.scene.config1_camera(W, H)
+    okw = {k: v for k, v in kw.items() if k != "kbuffer_depth"}
+    out = renderer.render(vi, pi, W, H, mode=mode, **kw)
+    ref = O.render(config1_enc, vi, pi, W, H, proxy_mode=1, **okw)
+    _cmp_images(out["rgba32f"], ref["rgba32f"])
+
+
 def test_camera_change_between_renders(renderer, gv, config1):
     """The handle re-uploads the camera matrices only when they change: alternating two cameras on one
     handle gives each camera's own image, equal to a fresh handle's."""
