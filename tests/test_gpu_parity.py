@@ -251,6 +251,23 @@ def test_render_params_vs_oracle(renderer, gv, O, config1, config1_enc, mode, kw
     _cmp_images(out["rgba32f"], ref["rgba32f"])
 
 
+@pytest.mark.parametrize("kmin", [0.0113, 0.05])
+def test_adaptive_kernel_clamping_vs_oracle(renderer, gv, O, config1, kmin):
+    """Enclosing opts = MOGRenderAdaptiveKernelClamping (particlePrimitives.comp:81-105): the proxy scale
+    follows each particle's density, so the render kernel recomputes it per record (ADAPTIVE template)."""
+    m = renderer.prepare(config1, kernel_min_response=kmin, opts=1)
+    e = O.enclose(config1, kernel_min_response=kmin, opts=1)
+    assert m == e["m"]
+    g = renderer.read_enclosing()
+    np.testing.assert_allclose(g["density"], e["density"][: 12 * m], rtol=1e-5, atol=1e-6)
+    W = H = 96
+    vi, pi = gv.scene.config1_camera(W, H)
+    for mode in (0, 1):
+        out = renderer.render(vi, pi, W, H, mode=mode)
+        ref = O.render(e, vi, pi, W, H, proxy_mode=1, kernel_min_response=kmin, kernel_opts=1)
+        _cmp_images(out["rgba32f"], ref["rgba32f"])
+
+
 def test_camera_change_between_renders(renderer, gv, config1):
     """The handle re-uploads the camera matrices only when they change: alternating two cameras on one
     handle gives each camera's own image, equal to a fresh handle's."""
