@@ -331,6 +331,9 @@ __device__ inline T sel4(T a0, T a1, T a2, T a3, uint32_t k) {  // values, not a
 #ifndef GVRT_ASM_NODE
 #define GVRT_ASM_NODE 1
 #endif
+#ifndef GVRT_SOFF
+#define GVRT_SOFF 1  // SGPR-offset node / record loads, inactive lanes excluded through tlo (no mask ANDs)
+#endif
 #if GVRT_ASM_NODE && GVRT_BVH_W == 4
 typedef int32_t sv16 __attribute__((ext_vector_type(16)));
 struct NodeS {
@@ -345,10 +348,28 @@ __device__ inline NodeS load_node(const Bvh4Node* __restrict__ p) {
                  : "s"(p));
     return n;
 }
+// node `idx` of the array at `base`: the 32-bit byte offset rides in the loads' SGPR offset field
+// (one shift instead of 64-bit pointer arithmetic per visit)
+__device__ inline NodeS load_node_at(const Bvh4Node* __restrict__ base, int32_t idx) {
+    NodeS n;
+    const uint32_t off = (uint32_t)idx << 7;
+    asm volatile("s_load_dwordx16 %0, %2, %3\n\ts_load_dwordx16 %1, %2, %3 offset:0x40\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(n.a), "=&s"(n.b)
+                 : "s"(base), "s"(off));
+    return n;
+}
+__device__ inline RenderRec load_rec_at(const RenderRec* __restrict__ base, int32_t idx) {
+    sv16 v;
+    const uint32_t off = (uint32_t)idx << 6;
+    asm volatile("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
+    return __builtin_bit_cast(RenderRec, v);
+}
 #define NODE_BOX(nd, k, j) (nd).f(6 * (k) + (j))
 #define NODE_CHILD(nd, k) (nd).w(24 + (k))
 #define NODE_PAD(nd, j) (nd).w(29 + (j))
 #else
+#undef GVRT_SOFF
+#define GVRT_SOFF 0
 typedef Bvh4Node NodeS;
 __device__ inline NodeS load_node(const Bvh4Node* __restrict__ p) { return *p; }
 #define NODE_BOX(nd, k, j) (nd).box[k][j]
@@ -525,7 +546,9 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
         if constexpr (LITERAL || STATS) {
             if (active) ++rounds;
         }
-        const float tlo = s_last[wid][lane] + EPS_T;
+        // (GVRT_SOFF: an inactive lane gets tlo = INF_DIST, so no box test of it can hit and the
+        // ballots need no AND with the active mask)
+        const float tlo = (!GVRT_SOFF || active) ? s_last[wid][lane] + EPS_T : INF_DIST;
         const float thi = s_tmax[wid][lane] + EPS_T;
 #pragma unroll
         for (int i = 0; i < KB; ++i) {
@@ -557,7 +580,11 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                 w_late += w_rounds > 1 ? 1u : 0u;
                 t_node0 = __builtin_amdgcn_s_memtime();  // the node phase includes the fetch
             }
+#if GVRT_SOFF
+            const NodeS nd = load_node_at(nodes_, unii(cur));  // whole node: 2x s_load_dwordx16 (4-wide)
+#else
             const NodeS nd = load_node(nodes_ + unii(cur));  // whole node: 2x s_load_dwordx16 (4-wide)
+#endif
             const float tc = fminf(fminf(thi, kt[KB - 1]), tcut);
             float ent[BVH_W];
             uint64_t bal[BVH_W];
@@ -570,7 +597,8 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                 const bool hit = box_hit(NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 1),
                                          NODE_BOX(nd, k, 3), NODE_BOX(nd, k, 5), o, oinv, inv, tlo, tc, ent[k]);
 #endif
-                bal[k] = __builtin_amdgcn_ballot_w64(hit) & amask;  // compare result straight to an SGPR mask
+                bal[k] = __builtin_amdgcn_ballot_w64(hit);  // compare result straight to an SGPR mask
+                if constexpr (!GVRT_SOFF) bal[k] &= amask;
             }
             int32_t ch[BVH_W];
 #pragma unroll
@@ -615,7 +643,11 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                 leafmask &= leafmask - 1;
                 const uint64_t bk = GVRT_PICK(bal, k);
                 const int32_t ck = GVRT_PICK(ch, k);
+#if GVRT_SOFF
+                const RenderRec rec = load_rec_at(recs_, unii(~ck));
+#else
                 const RenderRec rec = recs_[~ck];
+#endif
                 // split (SplitBLAS analogue): the piece's proxy id and cell; cell == ~0u admits every crossing
                 uint4 pa = make_uint4((uint32_t)(~ck), 0xFFFFFFFFu, 0u, 0u);
                 if (aux_) pa = aux_[~ck];
