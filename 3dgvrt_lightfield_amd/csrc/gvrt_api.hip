@@ -300,6 +300,9 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
     a.grid_inv = c->grid_inv;
     a.nodes = c->d_nodes4;
     a.nrecs = (uint32_t)c->m;
+    // the render kernel addresses leaf records (64 B) and 4-wide nodes (128 B) by 32-bit byte offsets
+    if (c->n_leaves >= (1ull << 26) || c->n_nodes4 >= (1ull << 25))
+        return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "more than 2^26 BVH leaves or 2^25 nodes (32-bit record offsets)");
     // cameras
     if ((s = ensure(c, (void**)&c->d_viewinv, &c->viewinv_cap, 64ull * ncams))) return s;
     // the camera matrices go up only when they changed (a pageable 64-B upload costs a host round trip
