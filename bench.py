@@ -37,6 +37,8 @@ def parse():
     ap.add_argument("--config", default="bicycle", choices=["bicycle", "garden", "truck", "lightfield", "config1"])
     ap.add_argument("--split", default="views", choices=["views", "tiles"])
     ap.add_argument("--mode", default="fast", choices=["fast", "literal"])
+    ap.add_argument("--ply", default=None, help="render this 3DGS .ply (e.g. Mip-NeRF360 bicycle) instead of the "
+                                                  "synthetic stand-in of --config (same camera and resolution)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true", help="skip the LITERAL stats pass (roofline bytes)")
@@ -61,7 +63,12 @@ def main():
     dev = torch.device("cuda", local_rank)
 
     gen, W, H, ncams_cfg = gv.scene.CONFIGS[args.config]
-    splats = gv.scene.make(**gen)
+    if args.ply:  # "if bicycle.ply is supplied, use it instead and say so"
+        splats = gv.SplatSet()
+        if not gv.PLYLoader().loadPLYModel(args.ply, splats):
+            raise SystemExit(f"cannot load {args.ply}")
+    else:
+        splats = gv.scene.make(**gen)
     n_input = splats["positions"].size // 3
 
     r = gv.Renderer(local_rank)
@@ -246,8 +253,9 @@ def main():
             "scaling": "weak" if args.split == "views" else "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded stand-in scene, SURVEY §8d)",
-            "config": {"workload": f"{args.config}: {n_input} synthetic Gaussians, {W}x{H}, "
+            "data": (f"real scene {os.path.basename(args.ply)}" if args.ply
+                     else "synthetic (seeded stand-in scene, SURVEY §8d)"),
+            "config": {"workload": f"{args.config}: {n_input} {'PLY' if args.ply else 'synthetic'} Gaussians, {W}x{H}, "
                                    f"{'one view per rank' if args.split == 'views' else 'one frame tile-split'}, "
                                    f"ray-query variant, {args.mode} k-buffer",
                        "gaussians": n_input, "survivors": m, "width": W, "height": H,

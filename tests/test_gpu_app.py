@@ -58,3 +58,18 @@ def test_app_eval_lightfield_hitcounts_bench(gv, tmp_path):
         fps, b = a.benchmark(vi, pi, 32, 32, warmup=0.05, duration=0.2, filename=str(tmp_path / "fps.txt"))
         assert fps > 0
         assert (tmp_path / "fps.txt").read_text().startswith("device,driverversion,duration (ms),frames,fps\n")
+
+
+def test_bench_on_a_ply(gv, tmp_path):
+    """bench.py --ply renders a supplied scene instead of the synthetic stand-in and says so."""
+    import subprocess
+    import sys
+    ply = str(tmp_path / "scene.ply")
+    gv.save_ply(ply, gv.scene.config1(n=5000))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--ply", ply, "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["data"] == "real scene scene.ply" and line["config"]["gaussians"] == 5000
+    assert line["value"] > 0 and line["roofline"]["frac"] > 0
