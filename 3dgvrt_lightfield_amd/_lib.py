@@ -96,6 +96,9 @@ SIGNATURES = {
     "gvrt_default_accel_params": (None, [_P(AccelParams)]),
     "gvrt_render": (C.c_int32, [H, _P(RenderParams), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
                                 C.c_uint32, C.c_void_p, C.c_uint64, _P(Image)]),
+    "gvrt_render_async": (C.c_int32, [H, _P(RenderParams), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                C.c_uint32, C.c_void_p, C.c_uint64, _P(Image)]),
+    "gvrt_sync": (C.c_int32, [H]),
     "gvrt_set_stats": (C.c_int32, [H, C.c_int]),
     "gvrt_get_stats": (C.c_int32, [H, _P(Stats)]),
     "gvrt_unpack_tiles_rgba8": (C.c_int32, [H, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,

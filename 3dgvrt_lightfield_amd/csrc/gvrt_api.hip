@@ -137,6 +137,7 @@ gvrt_status gvrt_destroy(gvrt_handle c) {
     for (auto& kv : c->allocs) ptrs.push_back(kv.first);
     for (void* p : ptrs) (void)hipFree(p);
     c->allocs.clear();
+    for (hipEvent_t e : c->async_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -265,10 +266,30 @@ static gvrt_status ensure(gvrt_context* c, void** p, uint64_t* cap, uint64_t byt
     return GVRT_OK;
 }
 
-gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float* view_inverse,
-                        const float* proj_inverse, uint32_t width, uint32_t height, uint32_t ncams,
-                        const gvrt_tile* tiles, uint64_t ntiles, const gvrt_image* out) {
+// Stream-ordered completion of the async launches since the last sync: their kernel times (HIP events)
+// averaged into stats.render_ms.
+static gvrt_status finish_async(gvrt_context* c) {
+    GVRT_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->async_pending) {
+        double sum = 0.0;
+        for (uint32_t k = 0; k < c->async_pending; ++k) {
+            float ms = 0.f;
+            GVRT_HIP(c, hipEventElapsedTime(&ms, c->async_ev[2 * k], c->async_ev[2 * k + 1]));
+            sum += ms;
+        }
+        c->stats.render_ms = (float)(sum / c->async_pending);
+        c->async_pending = 0;
+    }
+    return GVRT_OK;
+}
+
+static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const float* view_inverse,
+                               const float* proj_inverse, uint32_t width, uint32_t height, uint32_t ncams,
+                               const gvrt_tile* tiles, uint64_t ntiles, const gvrt_image* out, bool async) {
     if (!c) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL handle");
+    if (async && out && !out->device_ptrs)
+        return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "gvrt_render_async needs device output pointers");
+    if (async && c->stats_on) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "stats need the synchronous gvrt_render");
     if (!view_inverse || !proj_inverse || !out) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL argument");
     if (width == 0 || height == 0 || ncams == 0) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "empty image");
     if (width > 32768 || height > 32768 || ncams > 255)
@@ -309,6 +330,7 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
     // per frame for a static camera)
     if (c->h_viewinv.size() != 16ull * ncams ||
         std::memcmp(c->h_viewinv.data(), view_inverse, 64ull * ncams) != 0) {
+        if (c->async_pending) GVRT_HIP(c, hipStreamSynchronize(c->stream));  // an async upload may still read it
         c->h_viewinv.assign(view_inverse, view_inverse + 16ull * ncams);
         GVRT_HIP(c, hipMemcpyAsync(c->d_viewinv, c->h_viewinv.data(), 64ull * ncams, hipMemcpyHostToDevice, c->stream));
     }
@@ -344,7 +366,9 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
         return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "kbuffer_depth must be 0, 8, 12, 16, 20, 24 or 32");
     uint64_t nwork = total_tiles;
     if (tiles) {
-        std::vector<uint32_t> tl(ntiles);
+        if (c->async_pending) GVRT_HIP(c, hipStreamSynchronize(c->stream));  // h_tiles may feed a pending upload
+        std::vector<uint32_t>& tl = c->h_tiles;
+        tl.resize(ntiles);
         for (uint64_t i = 0; i < ntiles; ++i) {
             if (tiles[i].tx >= tiles_x || tiles[i].ty >= tiles_y || tiles[i].cam >= ncams)
                 return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "tile outside the image");
@@ -386,6 +410,24 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
         GVRT_HIP(c, hipMemsetAsync(c->d_stats, 0, 104, c->stream));
         a.stats = c->d_stats;
     }
+    if (async) {
+        // one event pair per queued launch, reused after every sync
+        if (2 * (c->async_pending + 1) > c->async_ev.size()) {
+            for (int k = 0; k < 2; ++k) {
+                hipEvent_t e = nullptr;
+                GVRT_HIP(c, hipEventCreate(&e));
+                c->async_ev.push_back(e);
+            }
+        }
+        hipEvent_t e0 = c->async_ev[2 * c->async_pending], e1 = c->async_ev[2 * c->async_pending + 1];
+        GVRT_HIP(c, hipEventRecord(e0, c->stream));
+        if ((s = gvrt_launch_render_mode(c, a, nwork, p->mode == GVRT_MODE_LITERAL))) return s;
+        GVRT_HIP(c, hipEventRecord(e1, c->stream));
+        ++c->async_pending;
+        c->stats.rays = (tiles || out->packed) ? nwork * 64 : total_tiles * 64;
+        return GVRT_OK;
+    }
+    if (c->async_pending && (s = finish_async(c))) return s;
     GVRT_HIP(c, hipEventRecord(c->ev0, c->stream));
     if ((s = gvrt_launch_render_mode(c, a, nwork, p->mode == GVRT_MODE_LITERAL))) return s;
     GVRT_HIP(c, hipEventRecord(c->ev1, c->stream));
@@ -415,14 +457,33 @@ gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float*
     return GVRT_OK;
 }
 
+gvrt_status gvrt_render(gvrt_handle c, const gvrt_render_params* p, const float* view_inverse,
+                        const float* proj_inverse, uint32_t width, uint32_t height, uint32_t ncams,
+                        const gvrt_tile* tiles, uint64_t ntiles, const gvrt_image* out) {
+    return render_impl(c, p, view_inverse, proj_inverse, width, height, ncams, tiles, ntiles, out, false);
+}
+
+gvrt_status gvrt_render_async(gvrt_handle c, const gvrt_render_params* p, const float* view_inverse,
+                              const float* proj_inverse, uint32_t width, uint32_t height, uint32_t ncams,
+                              const gvrt_tile* tiles, uint64_t ntiles, const gvrt_image* out) {
+    return render_impl(c, p, view_inverse, proj_inverse, width, height, ncams, tiles, ntiles, out, true);
+}
+
+gvrt_status gvrt_sync(gvrt_handle c) {
+    if (!c) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL handle");
+    GVRT_HIP(c, hipSetDevice(c->device));
+    return finish_async(c);
+}
+
 gvrt_status gvrt_unpack_tiles_rgba8(gvrt_handle c, const void* packed, const gvrt_tile* tiles, uint64_t ntiles,
                                     uint32_t width, uint32_t height, void* frame) {
     if (!c || !packed || !tiles || !frame) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL argument");
     GVRT_HIP(c, hipSetDevice(c->device));
+    gvrt_status s;
+    if (c->async_pending && (s = finish_async(c))) return s;  // queued renders may still read d_tiles
     std::vector<uint32_t> tl(ntiles);
     for (uint64_t i = 0; i < ntiles; ++i)
         tl[i] = ((uint32_t)tiles[i].cam << 24) | ((uint32_t)tiles[i].ty << 12) | tiles[i].tx;
-    gvrt_status s;
     if ((s = ensure(c, (void**)&c->d_tiles, &c->tiles_cap, 4 * (ntiles ? ntiles : 1)))) return s;
     if (ntiles) GVRT_HIP(c, hipMemcpyAsync(c->d_tiles, tl.data(), 4 * ntiles, hipMemcpyHostToDevice, c->stream));
     if ((s = gvrt_launch_unpack(c, packed, c->d_tiles, ntiles, width, height, frame))) return s;

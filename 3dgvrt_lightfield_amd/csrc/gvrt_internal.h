@@ -66,6 +66,9 @@ struct gvrt_context {
     float* d_viewinv = nullptr;
     uint64_t viewinv_cap = 0;
     std::vector<float> h_viewinv;  // host copy of what d_viewinv holds
+    std::vector<uint32_t> h_tiles; // host copy of the last tile list (source of an async upload)
+    std::vector<hipEvent_t> async_ev;  // event pairs of queued gvrt_render_async launches
+    uint32_t async_pending = 0;
     void* d_stage = nullptr;  // staging for host outputs
     uint64_t stage_cap = 0;
 

@@ -191,15 +191,21 @@ class Renderer:
         return out
 
     def render_device(self, view_inv, proj_inv, width, height, ncams=1, params=None, tiles=None, rgba8_ptr=None,
-                      rgba32f_ptr=None, ray_dirs_ptr=None, hit_counts_ptr=None, packed=False, **kw):
-        """Render into caller-owned device memory (e.g. torch tensor data_ptr())."""
+                      rgba32f_ptr=None, ray_dirs_ptr=None, hit_counts_ptr=None, packed=False, async_=False, **kw):
+        """Render into caller-owned device memory (e.g. torch tensor data_ptr()).  async_=True queues the
+        frame (gvrt_render_async) and returns at once; sync() waits for the queued frames."""
         p = params if params is not None else self.render_params(**kw)
         vi = np.ascontiguousarray(view_inv, np.float32).reshape(-1)
         pi = np.ascontiguousarray(proj_inv, np.float32).reshape(16)
         t, nt = self.tile_array(tiles)
         img = _lib.Image(rgba8_ptr, rgba32f_ptr, ray_dirs_ptr, hit_counts_ptr, 1, 1 if packed else 0)
-        check(lib().gvrt_render(self.h, C.byref(p), _lib.vptr(vi), _lib.vptr(pi), width, height, ncams,
-                                _lib.vptr(t), nt, C.byref(img)), self.h)
+        fn = lib().gvrt_render_async if async_ else lib().gvrt_render
+        check(fn(self.h, C.byref(p), _lib.vptr(vi), _lib.vptr(pi), width, height, ncams, _lib.vptr(t), nt,
+                 C.byref(img)), self.h)
+
+    def sync(self):
+        """gvrt_sync: wait for the frames queued by render_device(async_=True); render_ms() is then their mean."""
+        check(lib().gvrt_sync(self.h), self.h)
 
     def unpack_tiles_rgba8(self, packed_ptr, tiles, width, height, frame_ptr):
         t, nt = self.tile_array(tiles)

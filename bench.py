@@ -141,13 +141,19 @@ def main():
 
     it = [0]
 
+    # One GPU: frames are queued back to back (gvrt_render_async; one host round trip per K frames instead of
+    # one per frame); the kernel time is the mean over the queued launches (HIP event pairs), read at sync.
+    # Several ranks: synchronous renders, each frame handed to the RCCL gather as soon as it is done.
+    use_async = not distributed
+
     def step():
         b = it[0] % nbuf
         it[0] += 1
         finish(b)
         r.render_device(vi, pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=frames[b].data_ptr(),
-                        packed=args.split == "tiles")
-        kernel_ms.append(r.render_ms())
+                        packed=args.split == "tiles", async_=use_async)
+        if not use_async:
+            kernel_ms.append(r.render_ms())
         if distributed:
             if args.split == "views":
                 pending[b] = dist.gather(frames[b], gathered[b] if rank == 0 else None, dst=0, async_op=True)
@@ -162,6 +168,8 @@ def main():
     for _ in range(args.warmup):
         step()
     drain()
+    if use_async:
+        r.sync()
     kernel_ms.clear()
     if distributed:
         dist.barrier()
@@ -170,6 +178,9 @@ def main():
     for _ in range(args.steps):
         step()
     drain()  # every frame of the timed steps is rendered and gathered (and scattered) inside the clock
+    if use_async:
+        r.sync()  # every queued frame finished inside the clock
+        kernel_ms.append(r.render_ms())  # mean over the K launches
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()

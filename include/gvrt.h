@@ -183,6 +183,17 @@ gvrt_status gvrt_render(gvrt_handle h, const gvrt_render_params* p, const float*
                         uint32_t ncams, const gvrt_tile* tiles, uint64_t ntiles,
                         const gvrt_image* out);
 
+/* Asynchronous variant of gvrt_render (SURVEY §8b "an async variant plus gvrt_sync"): queues the
+ * launch on the handle's stream and returns; outputs must be device pointers and stats off.  Frames
+ * queued back to back run without a host round trip between them (the reference's per-frame
+ * vkQueueSubmit + fence, VulkanRTBase.cpp:983-1059).  gvrt_sync waits for every queued launch and sets
+ * stats.render_ms to their mean kernel time. */
+gvrt_status gvrt_render_async(gvrt_handle h, const gvrt_render_params* p, const float* view_inverse,
+                              const float* proj_inverse, uint32_t width, uint32_t height,
+                              uint32_t ncams, const gvrt_tile* tiles, uint64_t ntiles,
+                              const gvrt_image* out);
+gvrt_status gvrt_sync(gvrt_handle h);
+
 /* Enable per-render statistics (crossings/accepted/rounds; costs one atomic per wave). */
 gvrt_status gvrt_set_stats(gvrt_handle h, int enable);
 gvrt_status gvrt_get_stats(gvrt_handle h, gvrt_stats* s);

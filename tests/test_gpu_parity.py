@@ -286,6 +286,41 @@ def test_camera_change_between_renders(renderer, gv, config1):
         np.testing.assert_array_equal(r2.render(vib.reshape(-1), pi, W, H)["rgba32f"], b1)
 
 
+def test_async_render_queue(renderer, gv, config1):
+    """gvrt_render_async queues frames on the handle's stream (device outputs only, stats off); after
+    gvrt_sync each frame equals the synchronous render of its camera, and render_ms is the mean."""
+    torch = pytest.importorskip("torch")
+    renderer.prepare(config1)
+    W = H = 64
+    via, pi = gv.scene.config1_camera(W, H)
+    vib = np.array(via, np.float32).reshape(4, 4).copy()
+    vib[3, :3] += np.float32(0.3)
+    cams = [via, vib.reshape(-1), via, vib.reshape(-1)]
+    bufs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in cams]
+    for cam, b in zip(cams, bufs):
+        renderer.render_device(cam, pi, W, H, rgba32f_ptr=b.data_ptr(), async_=True)
+    renderer.sync()
+    assert renderer.render_ms() > 0
+    ref = [renderer.render(cam, pi, W, H)["rgba32f"][0] for cam in cams[:2]]
+    for k, b in enumerate(bufs):
+        np.testing.assert_array_equal(b.cpu().numpy(), ref[k % 2])
+    renderer.set_stats(True)
+    try:
+        with pytest.raises(gv.GvrtError):
+            renderer.render_device(via, pi, W, H, rgba32f_ptr=bufs[0].data_ptr(), async_=True)
+    finally:
+        renderer.set_stats(False)
+    # host outputs cannot be queued (the C-ABI refuses device_ptrs = 0)
+    import ctypes as C
+    L = gv.lib()
+    img = gv._lib.Image(None, C.c_void_p(bufs[0].data_ptr()), None, None, 0, 0)
+    p = renderer.render_params()
+    vi = np.ascontiguousarray(via, np.float32)
+    pf = np.ascontiguousarray(pi, np.float32).reshape(16)
+    st = L.gvrt_render_async(renderer.h, C.byref(p), gv._lib.vptr(vi), gv._lib.vptr(pf), W, H, 1, None, 0, C.byref(img))
+    assert st != 0
+
+
 # ------------------------------------------------------------------ full-size (bench scene) properties
 @pytest.fixture(scope="module")
 def bicycle(gv):
