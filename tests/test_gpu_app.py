@@ -73,3 +73,48 @@ def test_bench_on_a_ply(gv, tmp_path):
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["data"] == "real scene scene.ply" and line["config"]["gaussians"] == 5000
     assert line["value"] > 0 and line["roofline"]["frac"] > 0
+
+
+def test_cpp_app_flows_match_python(gv, tmp_path):
+    """The C++ gvrt_app (host/gvrt_host.cpp: PLYLoader, Camera, CameraLoader, vks::Benchmark, VulkanFullRT
+    flows) on the GPU: its frames equal the Python mirror's for the same cameras."""
+    Image = pytest.importorskip("PIL.Image")
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "3dgvrt_lightfield_amd", "gvrt_app")
+    splats = gv.scene.config1(n=3000)
+    ply = str(tmp_path / "scene.ply")
+    gv.save_ply(ply, splats)
+
+    def app_run(*args):
+        r = subprocess.run([exe, *args, "--ply", ply], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return r.stdout
+
+    W = H = 64
+    out = tmp_path / "cpp"
+    app_run("render", "--camera", "config1", "--width", str(W), "--height", str(H), "--out", str(out))
+    got = np.asarray(Image.open(out / "frame.png"))
+    with app.GvrtApp(0) as a:
+        a.prepare(ply=ply)
+        vi, pi = gv.scene.config1_camera(W, H)
+        ref = a.draw(vi, pi, W, H, rgba32f=False)["rgba8"][0]
+        assert (got != ref).any(axis=-1).mean() <= 1e-3  # camera matrices agree to float rounding
+        hc = a.hit_counts(vi, pi, W, H, str(tmp_path / "py_hits.txt"))
+        lf_ref = a.draw(*gv.camera.lightfield_ring_rig(a.splats["positions"], 4, 48, 48), 48, 48, ncams=4,
+                        rgba32f=False, pixel_offset=0.5, alpha_init=1.0)["rgba8"]
+    assert got[..., 3].max() > 0
+    app_run("hitcounts", "--camera", "config1", "--width", str(W), "--height", str(H), "--out", str(out))
+    rows = (out / "rayHitCountsOutput.txt").read_text().splitlines()
+    cpp_hc = np.array([[int(v) for v in r.split()] for r in rows])
+    assert (cpp_hc != hc).mean() <= 1e-3
+    app_run("lightfield", "--width", "48", "--height", "48", "--out", str(out / "lf"))
+    for c in range(4):
+        v = np.asarray(Image.open(out / "lf" / f"view_{c}.png"))
+        assert (v != lf_ref[c]).any(axis=-1).mean() <= 1e-3
+    d = np.fromfile(out / "lf" / "rayDirs.bin", np.float32).reshape(4, 48, 48, 4)
+    np.testing.assert_allclose(np.linalg.norm(d[..., :3], axis=-1), 1.0, atol=1e-5)
+    s = app_run("bench", "--camera", "config1", "--width", "32", "--height", "32", "--duration", "0.2", "--warmup", "0.05",
+                "--out", str(out))
+    assert "fps" in s
+    assert (out / "fps.txt").read_text().startswith("device,driverversion,duration (ms),frames,fps\n")
