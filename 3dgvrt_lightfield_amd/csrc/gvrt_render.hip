@@ -675,8 +675,10 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                             ico_clip(ok, dk, hk, tn, tf);
                             if (tn <= tf) {
                                 const float al = acc ? galpha : -1.0f;
-                                bool in0 = (a.tmin_inclusive ? tn >= tlo : tn > tlo) && tn <= thi;
-                                bool in1 = (a.tmin_inclusive ? tf >= tlo : tf > tlo) && tf <= thi;
+                                // (an inclusive tmin exists only in LITERAL mode: the API refuses it otherwise)
+                                const bool incl = LITERAL && a.tmin_inclusive;
+                                bool in0 = (incl ? tn >= tlo : tn > tlo) && tn <= thi;
+                                bool in1 = (incl ? tf >= tlo : tf > tlo) && tf <= thi;
                                 if (uni(pa.y) != 0xFFFFFFFFu) {
                                     in0 = in0 && crossing_cell(o, d, tn, a, pa.z, pa.w) == pa.y;
                                     in1 = in1 && crossing_cell(o, d, tf, a, pa.z, pa.w) == pa.y;

@@ -8,12 +8,15 @@ Tolerances (north star: "pixel-for-pixel within a stated float tolerance", PSNR 
     accepted-hit count (alpha channel) equal on >= 99.9 % of pixels
   * render vs the literal restatement (20-triangle soup, watertight triangle test): PSNR >= 50 dB
 """
+import os
+
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 RTOL, ATOL = 2e-6, 1e-7
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def _cmp_images(a, b, frac_tol=1e-3, max_tol=0.05, tol=2e-3):
@@ -266,6 +269,69 @@ def test_adaptive_kernel_clamping_vs_oracle(renderer, gv, O, config1, kmin):
         out = renderer.render(vi, pi, W, H, mode=mode)
         ref = O.render(e, vi, pi, W, H, proxy_mode=1, kernel_min_response=kmin, kernel_opts=1)
         _cmp_images(out["rgba32f"], ref["rgba32f"])
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13, 14, 15, 16])
+def test_random_scenes_and_cameras_vs_oracle(gv, O, seed):
+    """Seeded random scenes (size), frame sizes (ragged edges), camera positions, fields of view and
+    raygen variant: FAST and LITERAL images vs the oracle, LITERAL counters vs the oracle's."""
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(500, 6000))
+    s = gv.scene.config1(n=n, seed=seed)
+    W, H = int(rng.integers(17, 90)), int(rng.integers(17, 90))
+    u = rng.normal(size=3)
+    eye = tuple(float(x) for x in u / np.linalg.norm(u) * rng.uniform(0.6, 4.0))
+    vi, pi = gv.camera.pinhole(eye, (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), float(rng.uniform(20.0, 100.0)), W / H)
+    kw = dict(pixel_offset=0.5, alpha_init=1.0) if seed % 2 else {}
+    e = O.enclose(s)
+    ref = O.render(e, vi, pi, W, H, proxy_mode=1, **kw)
+    with gv.Renderer(0) as r:
+        assert r.prepare(s) == e["m"]
+        for mode in (gv.MODE_FAST, gv.MODE_LITERAL):
+            out = r.render(vi, pi, W, H, mode=mode, **kw)
+            _cmp_images(out["rgba32f"], ref["rgba32f"], frac_tol=2e-3)
+        r.set_stats(True)
+        r.render(vi, pi, W, H, mode=gv.MODE_LITERAL, **kw)
+        st = r.stats()
+    tot = ref["stats"].reshape(-1, 3).sum(axis=0)
+    assert abs(int(st["crossings"]) - int(tot[0])) <= 1e-3 * tot[0] + 2
+    assert abs(int(st["accepted"]) - int(tot[1])) <= 1e-3 * tot[1] + 2
+
+
+def test_hip_reproduces_golden_config1(renderer, gv, config1):
+    """The HIP path against the committed fixtures (tests/golden/make_golden.py): enclosing records,
+    the analytic-proxy image in both modes, the LITERAL counters, and the RT-variant image of the literal
+    20-triangle soup (PSNR, as the analytic clip and the triangle test differ at face edges)."""
+    z = np.load(os.path.join(GOLD, "config1_64.npz"))
+    assert renderer.prepare(config1) == int(z["m"][0])
+    g = renderer.read_enclosing()
+    np.testing.assert_array_equal(g["src_index"], z["src_index"])
+    np.testing.assert_allclose(g["density"][: z["density_head"].size], z["density_head"].reshape(-1), rtol=RTOL,
+                               atol=ATOL)
+    np.testing.assert_array_equal(g["sh"][: z["sh_head"].size], z["sh_head"].reshape(-1))
+    vi, pi = z["view_inv"], z["proj_inv"]
+    for mode in (gv.MODE_FAST, gv.MODE_LITERAL):
+        _cmp_images(renderer.render(vi, pi, 64, 64, mode=mode)["rgba32f"], z["rgba_analytic"])
+    renderer.set_stats(True)
+    try:
+        renderer.render(vi, pi, 64, 64, mode=gv.MODE_LITERAL)
+        st = renderer.stats()
+    finally:
+        renderer.set_stats(False)
+    tot = z["stats_analytic"].reshape(-1, 3).sum(axis=0)
+    assert abs(int(st["crossings"]) - int(tot[0])) <= 1e-3 * tot[0] + 2
+    assert abs(int(st["rounds"]) - int(tot[2])) <= 1e-3 * tot[2] + 2
+    rt = renderer.render(vi, pi, 64, 64, pixel_offset=0.5, alpha_init=1.0)
+    assert gv.psnr_rgb(rt["rgba8"], gv.quantize_rgba8(z["rgba_rt"])) >= 50.0
+
+
+def test_hip_reproduces_golden_lightfield(renderer, gv, config1):
+    z = np.load(os.path.join(GOLD, "lightfield_ring_24.npz"))
+    renderer.prepare(config1)
+    out = renderer.render(z["view_inv"], z["proj_inv"], 24, 24, ncams=4, pixel_offset=0.5, alpha_init=1.0,
+                          ray_dirs=True, ray_dirs_layout=1)
+    np.testing.assert_allclose(out["ray_dirs"].reshape(-1), z["ray_dirs"].reshape(-1), rtol=0, atol=2e-6)
+    assert gv.psnr_rgb(out["rgba8"], gv.quantize_rgba8(z["rgba"])) >= 50.0
 
 
 def test_camera_change_between_renders(renderer, gv, config1):
