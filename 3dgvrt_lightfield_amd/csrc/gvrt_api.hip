@@ -266,22 +266,32 @@ static gvrt_status ensure(gvrt_context* c, void** p, uint64_t* cap, uint64_t byt
     return GVRT_OK;
 }
 
-// Stream-ordered completion of the async launches since the last sync: their kernel times (HIP events)
-// averaged into stats.render_ms.
-static gvrt_status finish_async(gvrt_context* c) {
+// Stream-ordered completion of the async launches queued so far: their kernel times (HIP events) are
+// folded into a running sum, and the event pairs are free for reuse.
+static gvrt_status drain_async(gvrt_context* c) {
     GVRT_HIP(c, hipStreamSynchronize(c->stream));
-    if (c->async_pending) {
-        double sum = 0.0;
-        for (uint32_t k = 0; k < c->async_pending; ++k) {
-            float ms = 0.f;
-            GVRT_HIP(c, hipEventElapsedTime(&ms, c->async_ev[2 * k], c->async_ev[2 * k + 1]));
-            sum += ms;
-        }
-        c->stats.render_ms = (float)(sum / c->async_pending);
-        c->async_pending = 0;
+    for (uint32_t k = 0; k < c->async_pending; ++k) {
+        float ms = 0.f;
+        GVRT_HIP(c, hipEventElapsedTime(&ms, c->async_ev[2 * k], c->async_ev[2 * k + 1]));
+        c->async_ms_sum += ms;
     }
+    c->async_drained += c->async_pending;
+    c->async_pending = 0;
     return GVRT_OK;
 }
+
+// gvrt_sync: every async launch since the previous sync completed; stats.render_ms = their mean kernel time
+static gvrt_status finish_async(gvrt_context* c) {
+    gvrt_status s;
+    if ((s = drain_async(c))) return s;
+    if (c->async_drained) c->stats.render_ms = (float)(c->async_ms_sum / (double)c->async_drained);
+    c->async_ms_sum = 0.0;
+    c->async_drained = 0;
+    return GVRT_OK;
+}
+
+// a queue deeper than this many launches waits for the queued ones first (bounds the event pool)
+constexpr uint32_t MAX_ASYNC_PENDING = 1024;
 
 static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const float* view_inverse,
                                const float* proj_inverse, uint32_t width, uint32_t height, uint32_t ncams,
@@ -411,7 +421,8 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         a.stats = c->d_stats;
     }
     if (async) {
-        // one event pair per queued launch, reused after every sync
+        // one event pair per queued launch, reused after every drain
+        if (c->async_pending >= MAX_ASYNC_PENDING && (s = drain_async(c))) return s;
         if (2 * (c->async_pending + 1) > c->async_ev.size()) {
             for (int k = 0; k < 2; ++k) {
                 hipEvent_t e = nullptr;
@@ -427,7 +438,7 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         c->stats.rays = (tiles || out->packed) ? nwork * 64 : total_tiles * 64;
         return GVRT_OK;
     }
-    if (c->async_pending && (s = finish_async(c))) return s;
+    if ((c->async_pending || c->async_drained) && (s = finish_async(c))) return s;
     GVRT_HIP(c, hipEventRecord(c->ev0, c->stream));
     if ((s = gvrt_launch_render_mode(c, a, nwork, p->mode == GVRT_MODE_LITERAL))) return s;
     GVRT_HIP(c, hipEventRecord(c->ev1, c->stream));

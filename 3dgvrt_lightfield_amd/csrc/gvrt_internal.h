@@ -69,6 +69,8 @@ struct gvrt_context {
     std::vector<uint32_t> h_tiles; // host copy of the last tile list (source of an async upload)
     std::vector<hipEvent_t> async_ev;  // event pairs of queued gvrt_render_async launches
     uint32_t async_pending = 0;
+    double async_ms_sum = 0.0;         // kernel times of async launches drained before the next gvrt_sync
+    uint64_t async_drained = 0;
     void* d_stage = nullptr;  // staging for host outputs
     uint64_t stage_cap = 0;
 

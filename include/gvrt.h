@@ -187,7 +187,8 @@ gvrt_status gvrt_render(gvrt_handle h, const gvrt_render_params* p, const float*
  * launch on the handle's stream and returns; outputs must be device pointers and stats off.  Frames
  * queued back to back run without a host round trip between them (the reference's per-frame
  * vkQueueSubmit + fence, VulkanRTBase.cpp:983-1059).  gvrt_sync waits for every queued launch and sets
- * stats.render_ms to their mean kernel time. */
+ * stats.render_ms to their mean kernel time.  A queue of 1024 launches waits for them before queueing
+ * the next (bounded event pool). */
 gvrt_status gvrt_render_async(gvrt_handle h, const gvrt_render_params* p, const float* view_inverse,
                               const float* proj_inverse, uint32_t width, uint32_t height,
                               uint32_t ncams, const gvrt_tile* tiles, uint64_t ntiles,

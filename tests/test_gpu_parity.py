@@ -387,6 +387,26 @@ def test_async_render_queue(renderer, gv, config1):
     assert st != 0
 
 
+def test_async_queue_deeper_than_the_event_pool(renderer, gv, config1):
+    """More queued frames than the handle keeps event pairs for (1024): the queue drains itself, every
+    frame lands, and gvrt_sync's render_ms is still the mean over all of them."""
+    torch = pytest.importorskip("torch")
+    renderer.prepare(config1)
+    W = H = 16
+    vi, pi = gv.scene.config1_camera(W, H)
+    ref = renderer.render(vi, pi, W, H)["rgba32f"][0]
+    n = 1100
+    out = torch.zeros((n, H, W, 4), dtype=torch.float32, device="cuda")
+    for k in range(n):
+        renderer.render_device(vi, pi, W, H, rgba32f_ptr=out[k].data_ptr(), async_=True)
+    renderer.sync()
+    ms = renderer.render_ms()
+    assert 0 < ms < 50
+    o = out.cpu().numpy()
+    for k in (0, 1023, 1024, n - 1):
+        np.testing.assert_array_equal(o[k], ref)
+
+
 # ------------------------------------------------------------------ full-size (bench scene) properties
 @pytest.fixture(scope="module")
 def bicycle(gv):
