@@ -330,6 +330,7 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
     for (int k = 0; k < 3; ++k) a.grid_min[k] = c->grid_min[k];
     a.grid_inv = c->grid_inv;
     a.nodes = c->d_nodes4;
+    a.nodes64 = c->d_nodes64;
     a.nrecs = (uint32_t)c->m;
     // the render kernel addresses leaf records (64 B) and 4-wide nodes (128 B) by 32-bit byte offsets
     if (c->n_leaves >= (1ull << 26) || c->n_nodes4 >= (1ull << 25))

@@ -60,6 +60,24 @@ struct alignas(16) Bvh4Node {  // (name kept from the 4-wide layout; BVH_W child
 };
 static_assert(sizeof(Bvh4Node) == 28 * BVH_W + 16, "node layout: 128 B (4-wide) / 240 B (8-wide)");
 
+// Compressed 4-wide node (GVRT_NODE64 builds): 64 B, one s_load_dwordx16 per visit.  Child boxes are
+// f16 offsets from an f16 origin, rounded outward by one f16 ulp beyond the round-to-nearest result (the
+// origin sits 1/1024 of the node's extent below its box, so the outward step also covers the two-step
+// plane arithmetic of the traversal); the plane distance is one v_fma_mix_f32 from the SGPR halves,
+// as with the f32 layout.  Internal children are contiguous node ids and leaf children contiguous leaf
+// slots, both in slot order: one base index each instead of four child links.
+#ifndef GVRT_NODE64
+#define GVRT_NODE64 0
+#endif
+struct alignas(16) Node64 {
+    uint32_t box[4][3];    // [child][axis]: f16 lo | f16 hi << 16, offsets from the origin
+    uint32_t oxy;          // origin x | origin y << 16 (f16)
+    uint32_t oz_meta;      // origin z | meta << 16; meta = internal mask | valid mask << 4 | split axis << 8
+    uint32_t inner_base;   // node id of the first internal child
+    uint32_t leaf_base;    // leaf slot of the first leaf child
+};
+static_assert(sizeof(Node64) == 64, "Node64 must be 64 B");
+
 struct f3 {
     float x, y, z;
 };
@@ -80,6 +98,7 @@ struct RenderArgs {
     const float* __restrict__ sh;        // 48 f32 per k-buffer id
     const uint4* __restrict__ aux;       // split: per leaf {proxy, cell, cell range lo, hi}; else null
     const Bvh4Node* __restrict__ nodes;
+    const Node64* __restrict__ nodes64;  // GVRT_NODE64 builds
     const float* __restrict__ view_inv;  // 16 per camera, column-major
     const uint32_t* __restrict__ tiles;  // packed (cam<<24 | ty<<12 | tx) or null
     float proj_inv[16];

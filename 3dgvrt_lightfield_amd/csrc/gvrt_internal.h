@@ -48,6 +48,7 @@ struct gvrt_context {
     gvrt::BvhNode* d_nodes = nullptr;   // binary LBVH (kept for diagnostics)
     gvrt::Bvh4Node* d_nodes4 = nullptr; // 4-wide collapse traversed by the render kernel
     uint64_t n_nodes4 = 0;
+    gvrt::Node64* d_nodes64 = nullptr;  // GVRT_NODE64 builds: the compressed copy the render kernel reads
     uint32_t* d_leaf_src = nullptr;  // leaf -> compaction index
     uint64_t n_leaves = 0;           // BVH leaves: the survivors, or their split pieces
     uint32_t* d_leaf_aux = nullptr;  // split: per leaf {proxy, cell, proxy's cell range lo, hi} (uint4); else null

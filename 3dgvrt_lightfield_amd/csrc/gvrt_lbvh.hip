@@ -512,6 +512,121 @@ __global__ __launch_bounds__(256) void k_collapse_level(const BvhNode* __restric
     out[i] = o;
 }
 
+// ---- compressed 64-B nodes (GVRT_NODE64, layout in gvrt_device.h)
+__device__ inline uint16_t h16_bits(_Float16 h) { return __builtin_bit_cast(uint16_t, h); }
+__device__ inline float h16_val(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
+// neighbouring f16 toward -inf / +inf
+__device__ inline uint16_t h16_dn(uint16_t b) {
+    if ((b & 0x7FFFu) == 0) return 0x8001u;  // +-0 -> -smallest subnormal
+    return (b & 0x8000u) ? (uint16_t)(b + 1) : (uint16_t)(b - 1);
+}
+__device__ inline uint16_t h16_up(uint16_t b) {
+    if ((b & 0x7FFFu) == 0) return 0x0001u;
+    return (b & 0x8000u) ? (uint16_t)(b - 1) : (uint16_t)(b + 1);
+}
+// largest f16 <= x, then `extra` further steps down (ok cleared when the result is not finite)
+__device__ inline uint16_t f16_floor(float x, int extra, bool& ok) {
+    uint16_t b = h16_bits((_Float16)x);
+    if (!(h16_val(b) <= x)) b = h16_dn(b);
+    for (int i = 0; i < extra; ++i) b = h16_dn(b);
+    ok = ok && (b & 0x7C00u) != 0x7C00u && x == x;
+    return b;
+}
+__device__ inline uint16_t f16_ceil(float x, int extra, bool& ok) {
+    uint16_t b = h16_bits((_Float16)x);
+    if (!(h16_val(b) >= x)) b = h16_up(b);
+    for (int i = 0; i < extra; ++i) b = h16_up(b);
+    ok = ok && (b & 0x7C00u) != 0x7C00u && x == x;
+    return b;
+}
+
+// leaf children per node (the scan of these gives each node's first leaf slot)
+__global__ __launch_bounds__(256) void k_n64_count(uint64_t n4, const Bvh4Node* __restrict__ in, uint32_t* __restrict__ cnt) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n4) return;
+    uint32_t c = 0;
+    if (i < n4) {
+        const uint32_t nc = in[i].nchild;
+        for (uint32_t k = 0; k < nc && k < 4; ++k) c += in[i].child[k] < 0 ? 1u : 0u;
+    }
+    cnt[i] = c;
+}
+
+// one compressed node per 4-wide node; perm[leaf slot] = the leaf it holds (leaf order of the build)
+__global__ __launch_bounds__(256) void k_n64_emit(uint64_t n4, const Bvh4Node* __restrict__ in,
+                                                  const uint32_t* __restrict__ off, Node64* __restrict__ out,
+                                                  uint32_t* __restrict__ perm, uint32_t* __restrict__ err) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    const Bvh4Node n = in[i];
+    const uint32_t nc = n.nchild < 4 ? n.nchild : 4;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t k = 0; k < nc; ++k)
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = fminf(lo[a], n.box[k][2 * a]);
+            hi[a] = fmaxf(hi[a], n.box[k][2 * a + 1]);
+        }
+    bool ok = nc > 0;
+    uint16_t ob[3];
+    float org[3];
+    for (int a = 0; a < 3; ++a) {
+        const float ext = nc ? hi[a] - lo[a] : 0.0f;
+        ob[a] = f16_floor(nc ? lo[a] - ext * (1.0f / 1024.0f) : 0.0f, 0, ok);
+        org[a] = h16_val(ob[a]);
+    }
+    Node64 o;
+    uint32_t imask = 0, vmask = 0, ib = 0, ni = 0, nl = 0;
+    for (uint32_t k = 0; k < 4; ++k) {
+        if (k < nc) {
+            vmask |= 1u << k;
+            for (int a = 0; a < 3; ++a) {
+                const uint32_t l16 = f16_floor(n.box[k][2 * a] - org[a], 1, ok);
+                const uint32_t h16 = f16_ceil(n.box[k][2 * a + 1] - org[a], 1, ok);
+                o.box[k][a] = l16 | (h16 << 16);
+            }
+            const int32_t ch = n.child[k];
+            if (ch >= 0) {
+                imask |= 1u << k;
+                if (ni == 0) ib = (uint32_t)ch;
+                else ok = ok && (uint32_t)ch == ib + ni;  // internal children must be contiguous ids
+                ++ni;
+            } else {
+                perm[off[i] + nl] = (uint32_t)~ch;
+                ++nl;
+            }
+        } else {
+            for (int a = 0; a < 3; ++a) o.box[k][a] = 0u;
+        }
+    }
+    const uint32_t meta = imask | (vmask << 4) | ((n.pad[0] & 3u) << 8);
+    o.oxy = (uint32_t)ob[0] | ((uint32_t)ob[1] << 16);
+    o.oz_meta = (uint32_t)ob[2] | (meta << 16);
+    o.inner_base = ib;
+    o.leaf_base = off[i];
+    out[i] = o;
+    if (!ok) atomicOr(err, 1u);
+}
+
+// leaf data into the compressed tree's leaf-slot order
+__global__ __launch_bounds__(256) void k_n64_permute(uint64_t m, const uint32_t* __restrict__ perm,
+                                                     const RenderRec* __restrict__ rin, const float* __restrict__ shin,
+                                                     const uint32_t* __restrict__ srcin, const uint4* __restrict__ auxin,
+                                                     RenderRec* __restrict__ rout, float* __restrict__ shout,
+                                                     uint32_t* __restrict__ srcout, uint4* __restrict__ auxout) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const uint32_t t = perm[j];
+    rout[j] = rin[t];
+    if (shin) {
+        const float4* si = reinterpret_cast<const float4*>(shin + 48ull * t);
+        float4* so = reinterpret_cast<float4*>(shout + 48ull * j);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) so[k] = si[k];
+    }
+    srcout[j] = srcin[t];
+    if (auxin) auxout[j] = auxin[t];
+}
+
 }  // namespace
 
 // Surface-area-optimal 4-wide collapse (dynamic programming over the binary tree, after Ylitie, Karras
@@ -645,12 +760,87 @@ static gvrt_status host_dp_collapse(gvrt_context* c, int32_t root, uint64_t m, u
     return GVRT_OK;
 }
 
+#if GVRT_NODE64
+static_assert(BVH_W == 4, "compressed nodes are 4-wide");
+// Compressed copy of the 4-wide tree for the render kernel, with the leaf data (records, SH, leaf ->
+// compaction index, split aux) moved into leaf-slot order.
+static gvrt_status build_nodes64(gvrt_context* c, uint64_t m) {
+    const uint64_t n4 = c->n_nodes4;
+    uint32_t *cnt = nullptr, *off = nullptr, *perm = nullptr, *err = nullptr, *src2 = nullptr;
+    RenderRec* r2 = nullptr;
+    float* sh2 = nullptr;
+    uint32_t* aux2 = nullptr;
+    void* tmp = nullptr;
+    gvrt_status s = GVRT_OK;
+    auto fin = [&](gvrt_status st) {
+        gvrt_dfree(c, (void**)&cnt);
+        gvrt_dfree(c, (void**)&off);
+        gvrt_dfree(c, (void**)&perm);
+        gvrt_dfree(c, (void**)&err);
+        gvrt_dfree(c, &tmp);
+        gvrt_dfree(c, (void**)&r2);
+        gvrt_dfree(c, (void**)&sh2);
+        gvrt_dfree(c, (void**)&src2);
+        gvrt_dfree(c, (void**)&aux2);
+        return st;
+    };
+#define N64TRY(x)                                \
+    do {                                         \
+        if ((s = (x)) != GVRT_OK) return fin(s); \
+    } while (0)
+#define N64HIP(x, what)                                                \
+    do {                                                               \
+        hipError_t _e = (x);                                           \
+        if (_e != hipSuccess) return fin(gvrt_hip_check(c, _e, what)); \
+    } while (0)
+    gvrt_dfree(c, (void**)&c->d_nodes64);
+    N64TRY(gvrt_dalloc(c, (void**)&c->d_nodes64, sizeof(Node64) * (n4 ? n4 : 1)));
+    N64TRY(gvrt_dalloc(c, (void**)&cnt, 4 * (n4 + 1)));
+    N64TRY(gvrt_dalloc(c, (void**)&off, 4 * (n4 + 1)));
+    N64TRY(gvrt_dalloc(c, (void**)&perm, 4 * m));
+    N64TRY(gvrt_dalloc(c, (void**)&err, 4));
+    N64TRY(gvrt_dalloc(c, (void**)&r2, sizeof(RenderRec) * m));
+    N64TRY(gvrt_dalloc(c, (void**)&src2, 4 * m));
+    if (c->d_sh) N64TRY(gvrt_dalloc(c, (void**)&sh2, 192ull * m));
+    if (c->d_leaf_aux) N64TRY(gvrt_dalloc(c, (void**)&aux2, 16ull * m));
+    size_t tb = 0;
+    N64HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, off, (int)(n4 + 1), c->stream), "scan size");
+    N64TRY(gvrt_dalloc(c, &tmp, tb ? tb : 16));
+    N64HIP(hipMemsetAsync(err, 0, 4, c->stream), "memset");
+    hipLaunchKernelGGL(k_n64_count, dim3((unsigned)((n4 + 1 + 255) / 256)), dim3(256), 0, c->stream, n4, c->d_nodes4, cnt);
+    N64HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, off, (int)(n4 + 1), c->stream), "scan");
+    hipLaunchKernelGGL(k_n64_emit, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, c->stream, n4, c->d_nodes4, off,
+                       c->d_nodes64, perm, err);
+    N64HIP(hipGetLastError(), "k_n64_emit");
+    uint32_t h[2] = {0, 0};
+    N64HIP(hipMemcpyAsync(&h[0], err, 4, hipMemcpyDeviceToHost, c->stream), "err");
+    N64HIP(hipMemcpyAsync(&h[1], off + n4, 4, hipMemcpyDeviceToHost, c->stream), "leaves");
+    N64HIP(hipStreamSynchronize(c->stream), "sync");
+    if (h[0] || h[1] != m)
+        return fin(gvrt_fail(c, GVRT_ERR_UNSUPPORTED,
+                             "compressed nodes: coordinates beyond the f16 range, or a collapse whose internal "
+                             "children are not contiguous"));
+    hipLaunchKernelGGL(k_n64_permute, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, c->stream, m, perm, c->d_recs,
+                       c->d_sh, c->d_leaf_src, reinterpret_cast<const uint4*>(c->d_leaf_aux), r2, sh2, src2,
+                       reinterpret_cast<uint4*>(aux2));
+    N64HIP(hipGetLastError(), "k_n64_permute");
+    std::swap(c->d_recs, r2);
+    std::swap(c->d_leaf_src, src2);
+    if (sh2) std::swap(c->d_sh, sh2);
+    if (aux2) std::swap(c->d_leaf_aux, aux2);
+    return fin(GVRT_OK);  // frees the previous leaf-order buffers
+#undef N64TRY
+#undef N64HIP
+}
+#endif
+
 gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap) {
     const int64_t mp = (int64_t)c->m;  // proxies (survivors)
     gvrt_dfree(c, (void**)&c->d_recs);
     gvrt_dfree(c, (void**)&c->d_sh);
     gvrt_dfree(c, (void**)&c->d_nodes);
     gvrt_dfree(c, (void**)&c->d_nodes4);
+    gvrt_dfree(c, (void**)&c->d_nodes64);
     gvrt_dfree(c, (void**)&c->d_leaf_src);
     gvrt_dfree(c, (void**)&c->d_leaf_aux);
     c->n_nodes4 = 0;
@@ -869,7 +1059,7 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
         const int64_t ni = m - 1;
         const char* ce = getenv("GVRT_COLLAPSE");
         // the even-depth rule needs the Karras layout and 4-wide nodes
-        const bool greedy = ploc || BVH_W != 4 || !(ce && ce[0] == '0');
+        const bool greedy = ploc || BVH_W != 4 || GVRT_NODE64 || !(ce && ce[0] == '0');
         TRYH(hipGetLastError(), "k_karras");
         if ((ap.collapse == 1 || (ce && ce[0] == 'd')) && BVH_W == 4) {
             uint32_t d2 = 0, d4 = 0;
@@ -947,6 +1137,9 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
         c->n_nodes4 = n4;
         }
     }
+#if GVRT_NODE64
+    TRY(build_nodes64(c, (uint64_t)m));
+#endif
     TRYH(hipEventRecord(c->ev1, c->stream), "event");
     TRYH(hipStreamSynchronize(c->stream), "sync");
     float ms = 0.f;
