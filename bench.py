@@ -245,9 +245,17 @@ def main():
             t = time.perf_counter()
             ref = sc.render(vi[:16], pi, W, H, subset=sub, threads=threads)
             dt = time.perf_counter() - t
+            # and on one core, a strided sample sized for ~3 s
+            n1 = int(min(W * H, max(256, rate / threads * 3.0)))
+            sub1 = np.arange(0, W * H, max(1, (W * H) // n1), dtype=np.uint64)
+            t = time.perf_counter()
+            sc.render(vi[:16], pi, W, H, subset=sub1, threads=1)
+            dt1 = time.perf_counter() - t
             cpu = {"value": round(len(sub) / dt / 1e6, 6), "unit": "Mrays/s", "cores": threads, "kind": "port",
                    "sample": f"{len(sub)} rays (every {stride}th pixel of view 0), oracle analytic-proxy literal "
-                             f"ray-march, {dt:.1f} s on {threads} threads"}
+                             f"ray-march, {dt:.1f} s on {threads} threads",
+                   "value_1core": round(len(sub1) / dt1 / 1e6, 6),
+                   "sample_1core": f"{len(sub1)} rays (strided over view 0), {dt1:.1f} s on 1 thread"}
             img = r.render(vi[:16], pi, W, H, 1, params=params, rgba32f=True, rgba8=True)
             got = img["rgba8"].reshape(-1, 4)[sub.astype(np.int64)]
             psnr = gv.psnr_rgb(got, gv.quantize_rgba8(ref["rgba32f"]))
