@@ -235,7 +235,7 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
     gvrt_default_accel_params(&d);
     if (!p) p = &d;
     if (p->split_cells > 1023) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "split_cells must be <= 1023");
-    if (p->builder > 1) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "builder must be 0 (LBVH) or 1 (PLOC)");
+    if (p->builder > 2) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "builder must be 0 (LBVH), 1 (PLOC) or 2 (binned SAH, host)");
     if (p->collapse > 1) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "collapse must be 0 (greedy) or 1 (SAH-optimal DP)");
     GVRT_HIP(c, hipSetDevice(c->device));
     return gvrt_launch_build_accel(c, *p);

@@ -14,8 +14,11 @@
 //   7. depth census           (guards the render kernel's fixed LDS stack)
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <functional>
+#include <thread>
 #include <vector>
 
 #include "gvrt_internal.h"
@@ -641,6 +644,168 @@ static float host_area(const float* b) {
     return ex * ey + ey * ez + ez * ex;
 }
 
+// Binned-SAH binary BVH on the host (builder = 2, GVRT_BUILDER=sah): the trace-quality build of a
+// static scene, the counterpart of the reference's BLAS built once with
+// VK_BUILD_ACCELERATION_STRUCTURE_PREFER_FAST_TRACE_BIT_KHR (VulkanFullRT.cpp:575-787).  Top-down over
+// the Morton-ordered leaf boxes: per range, 32 centroid bins on each axis, the split of least
+// SA(left)·n(left) + SA(right)·n(right); an undecidable range (equal centroids) splits at its middle.
+// Nodes are written depth-first from the root (id 0) in the BvhNode layout the collapse reads: child 0 on
+// the lower side of the recorded split axis, leaves as ~(leaf index).
+static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lboxes, int32_t* root) {
+    std::vector<float> bx(6 * m);
+    GVRT_HIP(c, hipMemcpyAsync(bx.data(), d_lboxes, 24 * m, hipMemcpyDeviceToHost, c->stream));
+    GVRT_HIP(c, hipStreamSynchronize(c->stream));
+    std::vector<uint32_t> idx(m);
+    std::vector<float> cen(3 * m);
+    for (uint64_t i = 0; i < m; ++i) {
+        idx[i] = (uint32_t)i;
+        for (int a = 0; a < 3; ++a) cen[3 * i + a] = 0.5f * (bx[6 * i + a] + bx[6 * i + 3 + a]);
+    }
+    struct Box {
+        float lo[3], hi[3];
+        void reset() {
+            for (int a = 0; a < 3; ++a) { lo[a] = INFINITY; hi[a] = -INFINITY; }
+        }
+        void grow(const float* b) {
+            for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], b[a]); hi[a] = std::max(hi[a], b[3 + a]); }
+        }
+        void grow(const Box& b) {
+            for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], b.lo[a]); hi[a] = std::max(hi[a], b.hi[a]); }
+        }
+        float area() const {
+            if (!(hi[0] >= lo[0])) return 0.0f;
+            const float ex = hi[0] - lo[0], ey = hi[1] - lo[1], ez = hi[2] - lo[2];
+            return ex * ey + ey * ez + ez * ex;
+        }
+    };
+    constexpr int NB = 32;
+    // ids by range: the node of [b, e) is id, its left subtree (L leaves) takes ids id + 1 .. id + L - 1
+    // and the right child is id + L — independent of the order ranges are processed in, so subtrees
+    // build on several threads with the same result
+    std::vector<BvhNode> nodes(m - 1);
+    struct Task { uint32_t b, e, node; };
+    auto split = [&](const Task& t, Task* kids, int& nk) {
+        float cl[3] = {INFINITY, INFINITY, INFINITY}, ch[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (uint32_t i = t.b; i < t.e; ++i)
+            for (int a = 0; a < 3; ++a) {
+                cl[a] = std::min(cl[a], cen[3 * idx[i] + a]);
+                ch[a] = std::max(ch[a], cen[3 * idx[i] + a]);
+            }
+        int best_axis = -1, best_split = 0;
+        float best_cost = INFINITY;
+        for (int a = 0; a < 3; ++a) {
+            const float ext = ch[a] - cl[a];
+            if (!(ext > 0.0f)) continue;
+            const float sc = NB / ext;
+            Box bb[NB];
+            uint32_t bn[NB] = {};
+            for (int k = 0; k < NB; ++k) bb[k].reset();
+            for (uint32_t i = t.b; i < t.e; ++i) {
+                const int k = std::min(NB - 1, (int)((cen[3 * idx[i] + a] - cl[a]) * sc));
+                bb[k].grow(&bx[6ull * idx[i]]);
+                ++bn[k];
+            }
+            float rarea[NB];
+            uint32_t rcnt[NB];
+            Box acc;
+            acc.reset();
+            uint32_t n = 0;
+            for (int k = NB - 1; k > 0; --k) {
+                acc.grow(bb[k]);
+                n += bn[k];
+                rarea[k] = acc.area();
+                rcnt[k] = n;
+            }
+            acc.reset();
+            n = 0;
+            for (int k = 0; k < NB - 1; ++k) {  // split between bins k and k + 1
+                acc.grow(bb[k]);
+                n += bn[k];
+                if (n == 0 || rcnt[k + 1] == 0) continue;
+                const float cost = acc.area() * (float)n + rarea[k + 1] * (float)rcnt[k + 1];
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    best_axis = a;
+                    best_split = k;
+                }
+            }
+        }
+        uint32_t mid;
+        int axis;
+        if (best_axis >= 0) {
+            axis = best_axis;
+            const float sc = NB / (ch[axis] - cl[axis]);
+            const auto it = std::partition(idx.begin() + t.b, idx.begin() + t.e, [&](uint32_t p) {
+                return std::min(NB - 1, (int)((cen[3 * p + axis] - cl[axis]) * sc)) <= best_split;
+            });
+            mid = (uint32_t)(it - idx.begin());
+        } else {  // every centroid equal: halve the range
+            axis = 0;
+            mid = t.b + (t.e - t.b) / 2;
+        }
+        Box lb, rb;
+        lb.reset();
+        rb.reset();
+        for (uint32_t i = t.b; i < mid; ++i) lb.grow(&bx[6ull * idx[i]]);
+        for (uint32_t i = mid; i < t.e; ++i) rb.grow(&bx[6ull * idx[i]]);
+        BvhNode& nd = nodes[t.node];
+        float* nf = reinterpret_cast<float*>(&nd);
+        for (int a = 0; a < 3; ++a) {
+            nf[a] = lb.lo[a];
+            nf[3 + a] = lb.hi[a];
+            nf[6 + a] = rb.lo[a];
+            nf[9 + a] = rb.hi[a];
+        }
+        const uint32_t L = mid - t.b;
+        nk = 0;
+        if (L == 1) nd.c0 = ~(int32_t)idx[t.b];
+        else { nd.c0 = (int32_t)(t.node + 1); kids[nk++] = {t.b, mid, t.node + 1}; }
+        if (t.e - mid == 1) nd.c1 = ~(int32_t)idx[mid];
+        else { nd.c1 = (int32_t)(t.node + L); kids[nk++] = {mid, t.e, t.node + L}; }
+        nd.pad0 = (uint32_t)axis;
+        nd.pad1 = 0;
+    };
+    auto subtree = [&](Task root) {
+        std::vector<Task> st{root};
+        Task kids[2];
+        int nk = 0;
+        while (!st.empty()) {
+            const Task t = st.back();
+            st.pop_back();
+            split(t, kids, nk);
+            for (int k = 0; k < nk; ++k) st.push_back(kids[k]);
+        }
+    };
+    // the top of the tree breadth-first on this thread until there is work for every thread, then the
+    // subtrees on a small pool
+    const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<Task> front{{0u, (uint32_t)m, 0u}}, next;
+    while (!front.empty() && front.size() < 4 * nth) {
+        next.clear();
+        for (const Task& t : front) {
+            if (t.e - t.b < 4096) { next.push_back(t); continue; }
+            Task kids[2];
+            int nk = 0;
+            split(t, kids, nk);
+            for (int k = 0; k < nk; ++k) next.push_back(kids[k]);
+        }
+        if (next.size() == front.size()) { front.swap(next); break; }  // only small ranges left
+        front.swap(next);
+    }
+    std::atomic<size_t> cursor{0};
+    std::vector<std::thread> pool;
+    for (unsigned w = 0; w < nth; ++w)
+        pool.emplace_back([&]() {
+            for (size_t i; (i = cursor.fetch_add(1)) < front.size();) subtree(front[i]);
+        });
+    for (auto& th : pool) th.join();
+    GVRT_HIP(c, hipMemcpyAsync(c->d_nodes, nodes.data(), sizeof(BvhNode) * nodes.size(), hipMemcpyHostToDevice,
+                               c->stream));
+    GVRT_HIP(c, hipStreamSynchronize(c->stream));
+    *root = 0;
+    return GVRT_OK;
+}
+
 static gvrt_status host_dp_collapse(gvrt_context* c, int32_t root, uint64_t m, uint32_t* depth_out,
                                     uint32_t* depth4_out, uint64_t* n4_out) {
     const uint64_t ni = m - 1;
@@ -1037,10 +1202,13 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
         TRYH(hipMemsetAsync(dep, 0, 4, c->stream), "memset");
         const char* be = getenv("GVRT_BUILDER");
         const bool ploc = ap.builder == 1 || (be && be[0] == 'p');  // "ploc": measured 3 % slower to render (more visits), see DESIGN.md
+        const bool sah = !ploc && (ap.builder == 2 || (be && be[0] == 's'));
         int32_t root = 0;
         if (ploc) {
             uint32_t iters = 0;
             TRY(gvrt_ploc_build(c, (uint32_t)m, lboxes, c->d_nodes, lpar, npar, &root, &iters));
+        } else if (sah) {
+            TRY(host_sah_build(c, (uint64_t)m, lboxes, &root));
         } else {
             // leaf-range union table, then the hierarchy with its child boxes in one pass (no refit)
             hlv[0] = lboxes;
@@ -1059,7 +1227,7 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
         const int64_t ni = m - 1;
         const char* ce = getenv("GVRT_COLLAPSE");
         // the even-depth rule needs the Karras layout and 4-wide nodes
-        const bool greedy = ploc || BVH_W != 4 || GVRT_NODE64 || !(ce && ce[0] == '0');
+        const bool greedy = ploc || sah || BVH_W != 4 || GVRT_NODE64 || !(ce && ce[0] == '0');
         TRYH(hipGetLastError(), "k_karras");
         if ((ap.collapse == 1 || (ce && ce[0] == 'd')) && BVH_W == 4) {
             uint32_t d2 = 0, d4 = 0;

@@ -4,8 +4,9 @@ Gaussians; PSNR vs the reference restated by the CPU oracle).
 
 Workload at N=1: config 2 ("bicycle" stand-in, 1M synthetic Gaussians, seed 1, 1920x1080, orbit
 camera r=4 / elev 20 / fovy 50, ray-query variant).  A step = one Particle Rendering pass over one
-1920x1080 view with the scene, proxies and LBVH resident in HBM (enclosing + LBVH build are
-one-shot and reported separately).  With --gpus N each rank renders its own view of an N-camera
+1920x1080 view with the scene, proxies and BVH resident in HBM (enclosing + BVH build are
+one-shot and reported separately; by default the static-scene quality build, `--build fast` for the
+1.4 ms device LBVH).  With --gpus N each rank renders its own view of an N-camera
 light-field rig (config 5 shards views over GPUs) and the frames are gathered to rank 0 with RCCL
 (torch.distributed 'nccl'): per-GPU work is fixed, so scaling is weak.  `--split tiles` instead
 splits ONE frame into 64x64 blocks round-robin over ranks (strong scaling) and gathers the
@@ -42,6 +43,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true", help="skip the LITERAL stats pass (roofline bytes)")
+    ap.add_argument("--build", default="quality", choices=["quality", "fast"],
+                    help="quality: host binned-SAH tree + SAH-optimal 4-wide collapse (the static-scene build, as "
+                         "the reference's PREFER_FAST_TRACE BLAS); fast: device LBVH + greedy collapse (~1.4 ms)")
     return ap.parse_args()
 
 
@@ -72,9 +76,10 @@ def main():
     n_input = splats["positions"].size // 3
 
     r = gv.Renderer(local_rank)
-    m = r.prepare(splats)
+    bkw = dict(builder=2, collapse=1) if args.build == "quality" else {}
+    m = r.prepare(splats, **bkw)
     first_build = r.stats()  # includes the one-time lazy loading of the build kernels' code objects
-    m = r.prepare(splats)    # steady-state scene build (what a scene change costs)
+    m = r.prepare(splats, **bkw)    # steady-state scene build (what a scene change costs)
     st0 = r.stats()
 
     # cameras: an N-view planar rig around the config-2 orbit camera (view 0 = the config camera)
@@ -278,7 +283,9 @@ def main():
                                    f"{'one view per rank' if args.split == 'views' else 'one frame tile-split'}, "
                                    f"ray-query variant, {args.mode} k-buffer",
                        "gaussians": n_input, "survivors": m, "width": W, "height": H,
-                       "views": views, "split": args.split, "parallelism": f"{args.split}{world}"},
+                       "views": views, "split": args.split, "parallelism": f"{args.split}{world}",
+                       "build": ("quality: host binned-SAH tree + SAH-optimal 4-wide collapse" if args.build == "quality"
+                                 else "fast: device LBVH + greedy 4-wide collapse")},
             "fps": round(1e3 / ms_per_step, 2),
             "kernel_ms": round(kern_avg, 4),
             "kernel_mrays": round(rays_per_rank / (kern_avg * 1e-3) / 1e6, 3) if kern_avg == kern_avg else None,

@@ -155,7 +155,8 @@ gvrt_status gvrt_read_enclosing(gvrt_handle h, float* density12, float* sh48, fl
  * the scene's longest axis (the reference uses NUMBER_OF_CELLS_PER_LONGEST_AXIS = 10), every proxy
  * split into one piece per grid cell its box overlaps, each piece admitting only the crossings whose
  * point lies in its cell (so every crossing is found exactly once).  split_cells <= 1023 (0: no
- * split).  builder: 0 Karras LBVH, 1 PLOC.  collapse: 0 greedy surface-area 4-wide collapse on the
+ * split).  builder: 0 Karras LBVH, 1 PLOC, 2 binned SAH (host side; the PREFER_FAST_TRACE-style
+ * quality build of a static scene).  collapse: 0 greedy surface-area 4-wide collapse on the
  * device, 1 surface-area-optimal collapse (dynamic programming, host side: ~2.5 % fewer node visits,
  * tens of ms of build time). */
 typedef struct {

@@ -18,7 +18,8 @@ waves = (W + 7) // 8 * ((H + 7) // 8)
 rays = W * H
 out = {}
 with gv.Renderer(0) as r:
-    r.prepare(s, split_cells=int(os.environ.get("DIAG_SPLIT", "0")))
+    bkw = {} if os.environ.get("GVRT_BUILD") == "fast" else dict(builder=2, collapse=1)  # bench default
+    r.prepare(s, split_cells=int(os.environ.get("DIAG_SPLIT", "0")), **bkw)
     runs = [("literal", gv.MODE_LITERAL, 0)] + [(f"fast_k{k}", gv.MODE_FAST, k) for k in depths]
     for name, mode, k in runs:
         kw = dict(mode=mode, kbuffer_depth=k, rgba8=False, rgba32f=False)

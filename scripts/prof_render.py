@@ -9,7 +9,8 @@ gen, W, H, _ = gv.scene.CONFIGS[cfg]
 s = gv.scene.make(**gen)
 vi, pi = (gv.scene.mipnerf_camera(W, H) if cfg != "config1" else gv.scene.config1_camera(W, H))
 with gv.Renderer(0) as r:
-    r.prepare(s)
+    # the bench's default quality build (GVRT_BUILD=fast: device LBVH)
+    r.prepare(s, **({} if os.environ.get("GVRT_BUILD") == "fast" else dict(builder=2, collapse=1)))
     for _ in range(n):
         r.render(vi, pi, W, H, kbuffer_depth=k, rgba8=False, rgba32f=False)
     print("render_ms", r.stats()["render_ms"])
