@@ -678,13 +678,60 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
             return ex * ey + ey * ez + ez * ex;
         }
     };
-    constexpr int NB = 32;
+    // bins per axis (GVRT_SAH_BINS, default 32) and the range size at or below which the split is an exact
+    // sweep over the sorted centroids instead (GVRT_SAH_EXACT, default 0: binned everywhere)
+    constexpr int NBMAX = 128;
+    static const int NB = [] {
+        const char* e = getenv("GVRT_SAH_BINS");
+        const int v = e ? atoi(e) : 32;
+        return v < 4 ? 4 : (v > NBMAX ? NBMAX : v);
+    }();
+    static const uint32_t EXACT = [] {
+        const char* e = getenv("GVRT_SAH_EXACT");
+        return e ? (uint32_t)atoi(e) : 0u;
+    }();
     // ids by range: the node of [b, e) is id, its left subtree (L leaves) takes ids id + 1 .. id + L - 1
     // and the right child is id + L — independent of the order ranges are processed in, so subtrees
     // build on several threads with the same result
     std::vector<BvhNode> nodes(m - 1);
     struct Task { uint32_t b, e, node; };
     auto split = [&](const Task& t, Task* kids, int& nk) {
+        uint32_t mid = t.b + (t.e - t.b) / 2;
+        int axis = 0;
+        const uint32_t n_ = t.e - t.b;
+        if (n_ <= EXACT) {
+            std::vector<uint32_t> ord[3];
+            std::vector<float> ra(n_);
+            float best_cost = INFINITY;
+            int best_axis = -1;
+            uint32_t best_i = 0;
+            for (int a = 0; a < 3; ++a) {
+                ord[a].assign(idx.begin() + t.b, idx.begin() + t.e);
+                std::stable_sort(ord[a].begin(), ord[a].end(),
+                                 [&](uint32_t p, uint32_t q) { return cen[3 * p + a] < cen[3 * q + a]; });
+                Box acc;
+                acc.reset();
+                for (uint32_t i = n_ - 1; i >= 1; --i) {
+                    acc.grow(&bx[6ull * ord[a][i]]);
+                    ra[i] = acc.area();
+                }
+                acc.reset();
+                for (uint32_t i = 1; i < n_; ++i) {
+                    acc.grow(&bx[6ull * ord[a][i - 1]]);
+                    const float cost = acc.area() * (float)i + ra[i] * (float)(n_ - i);
+                    if (cost < best_cost) {
+                        best_cost = cost;
+                        best_axis = a;
+                        best_i = i;
+                    }
+                }
+            }
+            if (best_axis >= 0) {
+                std::copy(ord[best_axis].begin(), ord[best_axis].end(), idx.begin() + t.b);
+                axis = best_axis;
+                mid = t.b + best_i;
+            }
+        } else {
         float cl[3] = {INFINITY, INFINITY, INFINITY}, ch[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (uint32_t i = t.b; i < t.e; ++i)
             for (int a = 0; a < 3; ++a) {
@@ -697,16 +744,16 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
             const float ext = ch[a] - cl[a];
             if (!(ext > 0.0f)) continue;
             const float sc = NB / ext;
-            Box bb[NB];
-            uint32_t bn[NB] = {};
+            Box bb[NBMAX];
+            uint32_t bn[NBMAX] = {};
             for (int k = 0; k < NB; ++k) bb[k].reset();
             for (uint32_t i = t.b; i < t.e; ++i) {
                 const int k = std::min(NB - 1, (int)((cen[3 * idx[i] + a] - cl[a]) * sc));
                 bb[k].grow(&bx[6ull * idx[i]]);
                 ++bn[k];
             }
-            float rarea[NB];
-            uint32_t rcnt[NB];
+            float rarea[NBMAX];
+            uint32_t rcnt[NBMAX];
             Box acc;
             acc.reset();
             uint32_t n = 0;
@@ -730,8 +777,6 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
                 }
             }
         }
-        uint32_t mid;
-        int axis;
         if (best_axis >= 0) {
             axis = best_axis;
             const float sc = NB / (ch[axis] - cl[axis]);
@@ -739,9 +784,7 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
                 return std::min(NB - 1, (int)((cen[3 * p + axis] - cl[axis]) * sc)) <= best_split;
             });
             mid = (uint32_t)(it - idx.begin());
-        } else {  // every centroid equal: halve the range
-            axis = 0;
-            mid = t.b + (t.e - t.b) / 2;
+        }  // else every centroid equal: halve the range
         }
         Box lb, rb;
         lb.reset();
