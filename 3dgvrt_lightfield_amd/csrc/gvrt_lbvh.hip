@@ -651,7 +651,9 @@ static float host_area(const float* b) {
 // SA(left)·n(left) + SA(right)·n(right); an undecidable range (equal centroids) splits at its middle.
 // Nodes are written depth-first from the root (id 0) in the BvhNode layout the collapse reads: child 0 on
 // the lower side of the recorded split axis, leaves as ~(leaf index).
-static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lboxes, int32_t* root) {
+// keep != null: the tree stays on the host for the host-side collapse (no upload / download round trip)
+static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lboxes, int32_t* root,
+                                  std::vector<BvhNode>* keep) {
     std::vector<float> bx(6 * m);
     GVRT_HIP(c, hipMemcpyAsync(bx.data(), d_lboxes, 24 * m, hipMemcpyDeviceToHost, c->stream));
     GVRT_HIP(c, hipStreamSynchronize(c->stream));
@@ -842,18 +844,28 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
             for (size_t i; (i = cursor.fetch_add(1)) < front.size();) subtree(front[i]);
         });
     for (auto& th : pool) th.join();
+    *root = 0;
+    if (keep) {
+        keep->swap(nodes);
+        return GVRT_OK;
+    }
     GVRT_HIP(c, hipMemcpyAsync(c->d_nodes, nodes.data(), sizeof(BvhNode) * nodes.size(), hipMemcpyHostToDevice,
                                c->stream));
     GVRT_HIP(c, hipStreamSynchronize(c->stream));
-    *root = 0;
     return GVRT_OK;
 }
 
-static gvrt_status host_dp_collapse(gvrt_context* c, int32_t root, uint64_t m, uint32_t* depth_out,
+static gvrt_status host_dp_collapse(gvrt_context* c, int32_t root, uint64_t m, std::vector<BvhNode>* host_tree,
+                                    uint32_t* depth_out,
                                     uint32_t* depth4_out, uint64_t* n4_out) {
     const uint64_t ni = m - 1;
-    std::vector<BvhNode> bn(ni);
-    GVRT_HIP(c, hipMemcpyAsync(bn.data(), c->d_nodes, sizeof(BvhNode) * ni, hipMemcpyDeviceToHost, c->stream));
+    std::vector<BvhNode> bn;
+    if (host_tree && host_tree->size() == ni) {
+        bn.swap(*host_tree);
+    } else {
+        bn.resize(ni);
+        GVRT_HIP(c, hipMemcpyAsync(bn.data(), c->d_nodes, sizeof(BvhNode) * ni, hipMemcpyDeviceToHost, c->stream));
+    }
     GVRT_HIP(c, hipStreamSynchronize(c->stream));
     // F[n][k-1], k = 1..4, bottom-up by an explicit post-order walk
     std::vector<float> F(4 * ni, 0.0f);
@@ -1246,12 +1258,15 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
         const char* be = getenv("GVRT_BUILDER");
         const bool ploc = ap.builder == 1 || (be && be[0] == 'p');  // "ploc": measured 3 % slower to render (more visits), see DESIGN.md
         const bool sah = !ploc && (ap.builder == 2 || (be && be[0] == 's'));
+        const char* ce = getenv("GVRT_COLLAPSE");
+        const bool dp = (ap.collapse == 1 || (ce && ce[0] == 'd')) && BVH_W == 4;
+        std::vector<BvhNode> htree;  // SAH tree kept on the host for the DP collapse
         int32_t root = 0;
         if (ploc) {
             uint32_t iters = 0;
             TRY(gvrt_ploc_build(c, (uint32_t)m, lboxes, c->d_nodes, lpar, npar, &root, &iters));
         } else if (sah) {
-            TRY(host_sah_build(c, (uint64_t)m, lboxes, &root));
+            TRY(host_sah_build(c, (uint64_t)m, lboxes, &root, dp ? &htree : nullptr));
         } else {
             // leaf-range union table, then the hierarchy with its child boxes in one pass (no refit)
             hlv[0] = lboxes;
@@ -1268,14 +1283,13 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
                                (const float* const*)dlv);
         }
         const int64_t ni = m - 1;
-        const char* ce = getenv("GVRT_COLLAPSE");
         // the even-depth rule needs the Karras layout and 4-wide nodes
         const bool greedy = ploc || sah || BVH_W != 4 || GVRT_NODE64 || !(ce && ce[0] == '0');
         TRYH(hipGetLastError(), "k_karras");
-        if ((ap.collapse == 1 || (ce && ce[0] == 'd')) && BVH_W == 4) {
+        if (dp) {
             uint32_t d2 = 0, d4 = 0;
             uint64_t n4 = 0;
-            TRY(host_dp_collapse(c, root, m, &d2, &d4, &n4));
+            TRY(host_dp_collapse(c, root, m, &htree, &d2, &d4, &n4));
             c->depth = d2;
             c->depth4 = d4;
             c->n_nodes4 = n4;
