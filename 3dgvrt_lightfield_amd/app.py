@@ -239,6 +239,8 @@ def main(argv=None):
     ap.add_argument("--duration", type=float, default=10.0)
     ap.add_argument("--warmup", type=float, default=1.0)
     ap.add_argument("--frametimes", action="store_true")
+    ap.add_argument("--build", default="fast", choices=["fast", "quality"],
+                    help="fast: device LBVH (ms); quality: host binned SAH + SAH-optimal collapse (static scenes)")
     ap.add_argument("--split-cells", type=int, default=0,
                     help="SplitBLAS analogue: grid cells on the longest axis (reference: 10; 0 = off)")
     ap.add_argument("--gt", help="psnr: ground-truth folder")
@@ -254,7 +256,8 @@ def main(argv=None):
 
     kw = dict(pixel_offset=0.5, alpha_init=1.0) if args.variant == "rt" else {}
     with GvrtApp(0) as app:
-        m = app.prepare(ply=args.ply, config=args.config, split_cells=args.split_cells)
+        bkw = dict(builder=2, collapse=1) if args.build == "quality" else {}
+        m = app.prepare(ply=args.ply, config=args.config, split_cells=args.split_cells, **bkw)
         print(f"prepared: {m} Gaussians after the enclosing pass; stats {app.r.stats()}")
         if args.cmd == "eval":
             n = app.eval_capture(args.transforms, args.out, args.width, args.height, **kw)

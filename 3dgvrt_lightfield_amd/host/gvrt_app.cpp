@@ -76,7 +76,8 @@ int usage() {
     std::fprintf(stderr,
                  "usage: gvrt_app {render|eval|lightfield|hitcounts|bench|cameras|png} [--ply P] [--out D]\n"
                  "       [--width W] [--height H] [--camera orbit|config1] [--variant rq|rt] [--transforms T]\n"
-                 "       [--duration S] [--warmup S] [--frametimes] [--split-cells N] [--device I]\n");
+                 "       [--duration S] [--warmup S] [--frametimes] [--split-cells N] [--build fast|quality]\n"
+                 "       [--device I]\n");
     return 2;
 }
 
@@ -131,6 +132,10 @@ int main(int argc, char** argv) {
         gvrt_accel_params ap;
         gvrt_default_accel_params(&ap);
         ap.split_cells = (uint32_t)std::atoi(a.get("split-cells", "0").c_str());
+        if (a.get("build", "fast") == "quality") {  // static-scene build: host binned SAH + SAH-optimal collapse
+            ap.builder = 2;
+            ap.collapse = 1;
+        }
         const uint64_t m = app.prepare(ply, nullptr, &ap);
         const gvrt_stats st = app.stats();
         std::printf("prepared: %zu Gaussians, %llu after the enclosing pass; enclose %.3f ms, accel %.3f ms\n",
