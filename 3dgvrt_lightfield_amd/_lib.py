@@ -75,6 +75,18 @@ class Stats(C.Structure):
                 ("bvh_leaves", C.c_uint64), ("wave_rounds", C.c_uint64), ("wave_late_node_visits", C.c_uint64)]
 
 
+class DeviceProperties(C.Structure):
+    _fields_ = [("device_name", C.c_char * 256), ("driver_version", C.c_uint32), ("compute_units", C.c_uint32),
+                ("total_memory", C.c_uint64), ("arch_name", C.c_char * 64)]
+
+
+class DeviceBuffers(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("positions", C.c_void_p), ("rotations", C.c_void_p), ("scales", C.c_void_p),
+                ("densities", C.c_void_p), ("features_albedo", C.c_void_p), ("features_specular", C.c_void_p),
+                ("m", C.c_uint64), ("vertices", C.c_void_p), ("indices", C.c_void_p),
+                ("particle_density", C.c_void_p), ("particle_sph", C.c_void_p)]
+
+
 H = C.c_void_p
 _P = C.POINTER
 
@@ -100,9 +112,11 @@ SIGNATURES = {
                                 C.c_uint32, C.c_void_p, C.c_uint64, _P(Image)]),
     "gvrt_sync": (C.c_int32, [H]),
     "gvrt_set_stats": (C.c_int32, [H, C.c_int]),
+    "gvrt_get_device_properties": (C.c_int32, [C.c_int, _P(DeviceProperties)]),
+    "gvrt_get_device_buffers": (C.c_int32, [H, _P(DeviceBuffers)]),
     "gvrt_get_stats": (C.c_int32, [H, _P(Stats)]),
     "gvrt_unpack_tiles_rgba8": (C.c_int32, [H, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
-                                            C.c_void_p]),
+                                            C.c_uint32, C.c_void_p]),
     "gvrt_ply_load": (C.c_int32, [C.c_char_p, _P(SplatBuffers)]),
     "gvrt_ply_free": (None, [_P(SplatBuffers)]),
     "gvrt_ply_save": (C.c_int32, [C.c_char_p, _P(Splats)]),

@@ -23,7 +23,6 @@ CLI:  python -m 3dgvrt_lightfield_amd.app {render,eval,lightfield,hitcounts,benc
 """
 import argparse
 import importlib
-import math
 import os
 import sys
 import time
@@ -175,24 +174,20 @@ class GvrtApp:
 
     # EVAL_QUALITY capture
     def eval_capture(self, transforms_json, out_dir, width=800, height=800, **kw):
-        _, views = camera.load_nerf_cameras(transforms_json)
-        proj = camera.perspective_vulkan_no_depth_reverse(math.radians(camera.FOV_Y), width / height, camera.NEAR_PLANE,
-                                                          camera.FAR_PLANE)
-        pi = camera.colmajor(camera.inverse(proj))
+        vis, pi = camera.nerf_eval_matrices(transforms_json, width, height)  # setDatasetCamera per frame
         os.makedirs(out_dir, exist_ok=True)
-        for i, w2c in enumerate(views):
-            vi = camera.colmajor(camera.inverse(w2c))
+        for i, vi in enumerate(vis):
             img = self.draw(vi, pi, width, height, rgba32f=False, **kw)["rgba8"][0]
             save_png(os.path.join(out_dir, f"r_{i}.png"), img)
-        return len(views)
+        return len(vis)
 
     def light_field(self, out_dir, rig="ring", width=180, height=180, **kw):
         if rig == "ring":  # computeGaussianLightField: RT-pipeline semantics (+0.5, alpha 1)
             vi, pi = camera.lightfield_ring_rig(self.splats["positions"], 4, width, height)
             kw = dict(dict(pixel_offset=0.5, alpha_init=1.0), **kw)
         else:  # config 5 grid
-            vi, pi = camera.lightfield_grid_rig((4.0 * math.cos(math.radians(20.0)), 4.0 * math.sin(math.radians(20.0)), 0.0),
-                                                (0.0, 0.0, 0.0), nx=4, ny=4, spacing=0.1, aspect=width / height)
+            vi, pi = camera.lightfield_grid_rig(camera.orbit_eye(4.0, 20.0, 90.0), (0.0, 0.0, 0.0), nx=4, ny=4,
+                                                spacing=0.1, aspect=camera.aspect_ratio(width, height))
         ncams = len(vi) // 16
         out = self.draw(vi, pi, width, height, ncams=ncams, rgba32f=False, ray_dirs=True, ray_dirs_layout=1, **kw)
         os.makedirs(out_dir, exist_ok=True)
@@ -211,8 +206,8 @@ class GvrtApp:
         torch = importlib.import_module("torch")  # device buffer + synchronize (plumbing)
         frame = torch.empty((height, width, 4), dtype=torch.uint8, device="cuda")
         b = Benchmark(warmup, duration, filename, frame_times)
-        props = torch.cuda.get_device_properties(0)
-        b.device, b.driver = props.name.replace(",", " "), str(torch.version.hip)
+        props = gv.device_properties(self.r.device)  # the deviceName / driverVersion fps.txt reports
+        b.device, b.driver = props["device_name"].replace(",", " "), str(props["driver_version"])
         fps = b.run(lambda: self.r.render_device(view_inv, proj_inv, width, height, rgba8_ptr=frame.data_ptr(), **kw),
                     torch.cuda.synchronize)
         b.save_results()

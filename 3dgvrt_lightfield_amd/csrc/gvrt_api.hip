@@ -58,7 +58,7 @@ extern "C" {
 int gvrt_abi_version(void) { return GVRT_ABI_VERSION; }
 
 const char* gvrt_build_info(void) {
-    return "gvrt " "abi1 gfx950 hip" " (" __DATE__ " " __TIME__ ")";
+    return "gvrt " "abi2 gfx950 hip" " (" __DATE__ " " __TIME__ ")";
 }
 
 void gvrt_default_enclosing_params(gvrt_enclosing_params* p) {
@@ -162,14 +162,18 @@ gvrt_status gvrt_load_splats(gvrt_handle c, const gvrt_splats* s) {
     c->enclosed = false;
     c->accel = false;
     c->m = 0;
+    c->n = 0;  // the handle holds no splats until every buffer below exists
+    c->stats.n_input = 0;
     const uint64_t n = s->n;
-    gvrt_status st;
-    if ((st = gvrt_dalloc(c, (void**)&c->d_pos, 12 * n))) return st;
-    if ((st = gvrt_dalloc(c, (void**)&c->d_rot, 16 * n))) return st;
-    if ((st = gvrt_dalloc(c, (void**)&c->d_scl, 12 * n))) return st;
-    if ((st = gvrt_dalloc(c, (void**)&c->d_opa, 4 * n))) return st;
-    if ((st = gvrt_dalloc(c, (void**)&c->d_fdc, 12 * n))) return st;
-    if ((st = gvrt_dalloc(c, (void**)&c->d_frest, 180 * n + 360))) return st;
+    gvrt_status st = GVRT_OK;
+    float** bufs[6] = {&c->d_pos, &c->d_rot, &c->d_scl, &c->d_opa, &c->d_fdc, &c->d_frest};
+    const uint64_t bytes[6] = {12 * n, 16 * n, 12 * n, 4 * n, 12 * n, 180 * n + 360};
+    for (int i = 0; i < 6 && st == GVRT_OK; ++i) st = gvrt_dalloc(c, (void**)bufs[i], bytes[i]);
+    if (st != GVRT_OK) {  // no half-loaded state: a later build sees "not loaded", never a short buffer
+        std::string msg = c->err;
+        for (float** b : bufs) gvrt_dfree(c, (void**)b);
+        return gvrt_fail(c, st, msg);
+    }
     if (n) {
         GVRT_HIP(c, hipMemcpyAsync(c->d_pos, s->positions, 12 * n, hipMemcpyHostToDevice, c->stream));
         GVRT_HIP(c, hipMemcpyAsync(c->d_rot, s->rotation, 16 * n, hipMemcpyHostToDevice, c->stream));
@@ -190,7 +194,8 @@ gvrt_status gvrt_build_enclosing(gvrt_handle c, const gvrt_enclosing_params* p, 
     gvrt_enclosing_params def;
     gvrt_default_enclosing_params(&def);
     if (!p) p = &def;
-    if (!c->d_pos) return gvrt_fail(c, GVRT_ERR_STATE, "gvrt_load_splats has not been called");
+    if (!c->d_pos || !c->d_rot || !c->d_scl || !c->d_opa || !c->d_fdc || !c->d_frest)
+        return gvrt_fail(c, GVRT_ERR_STATE, "gvrt_load_splats has not been called");
     GVRT_HIP(c, hipSetDevice(c->device));
     uint64_t mm = 0;
     gvrt_status s = gvrt_launch_enclose(c, p, &mm);
@@ -242,6 +247,49 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
 }
 
 gvrt_status gvrt_build_accel(gvrt_handle c) { return gvrt_build_accel_ex(c, nullptr); }
+
+gvrt_status gvrt_get_device_properties(int device, gvrt_device_properties* out) {
+    if (!out) return gvrt_fail(nullptr, GVRT_ERR_INVALID_ARG, "out is NULL");
+    std::memset(out, 0, sizeof(*out));
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+        (void)hipGetLastError();
+        return gvrt_fail(nullptr, GVRT_ERR_NO_DEVICE, "no HIP device available");
+    }
+    if (device < 0 || device >= n) return gvrt_fail(nullptr, GVRT_ERR_INVALID_ARG, "device index out of range");
+    hipDeviceProp_t prop{};
+    hipError_t e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) return gvrt_hip_check(nullptr, e, "hipGetDeviceProperties");
+    std::snprintf(out->device_name, sizeof(out->device_name), "%s", prop.name);
+    std::snprintf(out->arch_name, sizeof(out->arch_name), "%s", prop.gcnArchName);
+    out->compute_units = (uint32_t)prop.multiProcessorCount;
+    out->total_memory = (uint64_t)prop.totalGlobalMem;
+    int drv = 0;
+    if (hipDriverGetVersion(&drv) == hipSuccess) out->driver_version = (uint32_t)drv;
+    return GVRT_OK;
+}
+
+gvrt_status gvrt_get_device_buffers(gvrt_handle c, gvrt_device_buffers* out) {
+    if (!c || !out) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL argument");
+    std::memset(out, 0, sizeof(*out));
+    out->n = c->n;
+    out->positions = c->d_pos;
+    out->rotations = c->d_rot;
+    out->scales = c->d_scl;
+    out->densities = c->d_opa;
+    out->features_albedo = c->d_fdc;
+    out->features_specular = c->d_frest;
+    if (c->enclosed) {
+        out->m = c->m;
+        out->particle_density = c->d_density12;
+        out->particle_sph = c->d_sh48;
+        if (c->enc.emit_triangles) {
+            out->vertices = c->d_verts;
+            out->indices = c->d_tris;
+        }
+    }
+    return GVRT_OK;
+}
 
 gvrt_status gvrt_set_stats(gvrt_handle c, int enable) {
     if (!c) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL handle");
@@ -488,14 +536,20 @@ gvrt_status gvrt_sync(gvrt_handle c) {
 }
 
 gvrt_status gvrt_unpack_tiles_rgba8(gvrt_handle c, const void* packed, const gvrt_tile* tiles, uint64_t ntiles,
-                                    uint32_t width, uint32_t height, void* frame) {
+                                    uint32_t width, uint32_t height, uint32_t ncams, void* frame) {
     if (!c || !packed || !tiles || !frame) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL argument");
+    if (width == 0 || height == 0 || width > 32768 || height > 32768 || ncams == 0 || ncams > 255)
+        return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "frame must be 1..32768 pixels per side, 1..255 cameras");
+    const uint32_t tiles_x = (width + 7) / 8, tiles_y = (height + 7) / 8;
+    std::vector<uint32_t> tl(ntiles);
+    for (uint64_t i = 0; i < ntiles; ++i) {  // the packed tile word carries tx, ty in 12 bits and cam in 8
+        if (tiles[i].tx >= tiles_x || tiles[i].ty >= tiles_y || tiles[i].cam >= ncams)
+            return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "tile outside the frame");
+        tl[i] = ((uint32_t)tiles[i].cam << 24) | ((uint32_t)tiles[i].ty << 12) | tiles[i].tx;
+    }
     GVRT_HIP(c, hipSetDevice(c->device));
     gvrt_status s;
     if (c->async_pending && (s = finish_async(c))) return s;  // queued renders may still read d_tiles
-    std::vector<uint32_t> tl(ntiles);
-    for (uint64_t i = 0; i < ntiles; ++i)
-        tl[i] = ((uint32_t)tiles[i].cam << 24) | ((uint32_t)tiles[i].ty << 12) | tiles[i].tx;
     if ((s = ensure(c, (void**)&c->d_tiles, &c->tiles_cap, 4 * (ntiles ? ntiles : 1)))) return s;
     if (ntiles) GVRT_HIP(c, hipMemcpyAsync(c->d_tiles, tl.data(), 4 * ntiles, hipMemcpyHostToDevice, c->stream));
     if ((s = gvrt_launch_unpack(c, packed, c->d_tiles, ntiles, width, height, frame))) return s;

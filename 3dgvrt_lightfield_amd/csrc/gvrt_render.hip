@@ -67,6 +67,31 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 #ifndef GVRT_VSTACK
 #define GVRT_VSTACK 0
 #endif
+// GVRT_TRACE=1 (debug builds only, `make variant V=trace FLAGS=-DGVRT_TRACE=1`): the lane of one chosen
+// pixel records its crossings (kind 1: id, tn, tf, accepted, alpha, round), composites (kind 2: id, t,
+// alpha, T before, accepted, round) and round starts (kind 3: tlo, thi, T, qneed) to a device buffer,
+// read back with gvrt_debug_trace_get (declared only in this build).
+#ifndef GVRT_TRACE
+#define GVRT_TRACE 0
+#endif
+#if GVRT_TRACE
+__device__ float g_trace[8 * 8192];
+__device__ unsigned int g_trace_n;
+__device__ unsigned long long g_trace_pix;
+#define GVRT_TRACE_REC(on, k, x0, x1, x2, x3, x4, x5)                                   \
+    do {                                                                                \
+        if (on) {                                                                       \
+            const unsigned int ti = atomicAdd(&g_trace_n, 1u);                          \
+            if (ti < 8192) {                                                            \
+                float* tr = g_trace + 8 * ti;                                           \
+                tr[0] = (float)(k); tr[1] = (float)(x0); tr[2] = (x1); tr[3] = (x2);     \
+                tr[4] = (x3); tr[5] = (x4); tr[6] = (float)(x5); tr[7] = 0.0f;          \
+            }                                                                           \
+        }                                                                               \
+    } while (0)
+#else
+#define GVRT_TRACE_REC(on, k, x0, x1, x2, x3, x4, x5) do { } while (0)
+#endif
 #ifndef GVRT_APPROX_RESPONSE
 #define GVRT_APPROX_RESPONSE 1
 #endif
@@ -470,6 +495,9 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
     cam = uni(cam);
     const uint32_t px = tx * 8 + (lane & 7), py = ty * 8 + (lane >> 3);
     const bool valid = px < a.width && py < a.height && cam < a.ncams;
+#if GVRT_TRACE
+    const bool trace_on = valid && ((uint64_t)cam * a.height + py) * a.width + px == g_trace_pix;
+#endif
 
     // ---- ray generation (particleRendering.comp:123-129, raygen.rgen:116-121)
     const float* V = view_inv_ + 16 * (cam < a.ncams ? cam : 0);
@@ -592,6 +620,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
             qneed = (uint32_t)fminf(ceilf(need), 4.0e9f);
         }
         uint32_t qtot = 0;  // PACK: sum of the q codes inserted this round (>= the buffer's sum)
+        GVRT_TRACE_REC(trace_on && active, 3, 0, tlo, thi, s_T[wid][lane], (float)qneed, rounds);
 
         // ---------------- trace(): packet traversal of the 4-wide LBVH
         float tcut = INF_DIST;  // termination-aware cull distance of this lane (see the leaf insert)
@@ -736,6 +765,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                                 ADAPTIVE ? kernel_scale(rec.density, a.kmin, a.kopts, a.kdeg) * SQRT3 : a.kernel_h;
                             float tn, tf;
                             ico_clip(ok, dk, hk, tn, tf);
+                            GVRT_TRACE_REC(trace_on, 1, gi, tn, tf, acc ? 1.0f : 0.0f, galpha, rounds);
                             if (tn <= tf) {
                                 const float al = acc ? galpha : -1.0f;
                                 // (an inclusive tmin exists only in LITERAL mode: the API refuses it otherwise)
@@ -845,6 +875,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                             halpha = ka[j];
                             hacc = ka[j] > 0.0f;
                         }
+                        GVRT_TRACE_REC(trace_on, 2, hid, kt[j], halpha, T, hacc ? 1.0f : 0.0f, rounds);
                         if (hacc) {
                             const float weight = halpha * T;
                             float rr = 0.f, rg = 0.f, rb = 0.f;
@@ -1010,6 +1041,22 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
     GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;
 }
+
+#if GVRT_TRACE
+extern "C" int gvrt_debug_trace_set(unsigned long long pix) {
+    const unsigned int z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_trace_pix), &pix, sizeof(pix)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_trace_n), &z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+extern "C" int gvrt_debug_trace_get(float* out, int maxn) {
+    unsigned int n = 0;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_trace_n), sizeof(n)) != hipSuccess) return -1;
+    const int m = (int)(n < 8192u ? n : 8192u) < maxn ? (int)(n < 8192u ? n : 8192u) : maxn;
+    if (m > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace), sizeof(float) * 8 * m) != hipSuccess) return -1;
+    return (int)n;
+}
+#endif
 
 gvrt_status gvrt_launch_unpack(gvrt_context* c, const void* packed, const uint32_t* tiles, uint64_t ntiles,
                                uint32_t width, uint32_t height, void* frame) {

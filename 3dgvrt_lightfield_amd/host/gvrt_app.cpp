@@ -21,7 +21,9 @@
 
 #include "gvrt_host.h"
 
-using namespace gvrt_host;
+using gvrt_host::GvrtApp;
+using gvrt_host::preset_camera;
+using gvrt_host::write_png;
 
 namespace {
 
@@ -51,25 +53,21 @@ Args parse(int argc, char** argv) {
     return a;
 }
 
-// the presets of the Python app / bench: config-1 pinhole and the config-2 orbit camera
-Camera preset_camera(const std::string& name, uint32_t w, uint32_t h) {
-    Camera c;
-    if (name == "config1") {
-        c.setLookAt({0.0, 0.0, 3.0}, {0.0, 0.0, 0.0}, {0.0, 1.0, 0.0});
-        c.setPerspective(FOV_Y, (double)w / h, NEAR_PLANE, FAR_PLANE);
-    } else {
-        const double el = 20.0 * M_PI / 180.0, az = 30.0 * M_PI / 180.0, r = 4.0;
-        c.setLookAt({r * std::cos(el) * std::sin(az), r * std::sin(el), r * std::cos(el) * std::cos(az)},
-                    {0.0, 0.0, 0.0}, {0.0, 1.0, 0.0});
-        c.setPerspective(50.0, (double)w / h, NEAR_PLANE, FAR_PLANE);
+// matrices as 16 uint32 hex words in glm memory order (bit-exact comparison with the reference's)
+void print_mat(const std::string& name, const gm::mat4& m) {
+    std::printf("%s", name.c_str());
+    for (int i = 0; i < 16; ++i) {
+        uint32_t u;
+        std::memcpy(&u, m.data() + i, 4);
+        std::printf(" %08x", u);
     }
-    return c;
+    std::printf("\n");
 }
 
-void print_mat(const char* name, const std::array<float, 16>& m) {
-    std::printf("%s", name);
-    for (float v : m) std::printf(" %.9g", v);
-    std::printf("\n");
+gm::vec3 parse_vec3(const std::string& s) {
+    gm::vec3 v;
+    if (std::sscanf(s.c_str(), "%f,%f,%f", &v.x, &v.y, &v.z) != 3) throw std::runtime_error("expected x,y,z: " + s);
+    return v;
 }
 
 int usage() {
@@ -102,22 +100,38 @@ int main(int argc, char** argv) {
                 }
             return write_png(out, img.data(), W, H) ? 0 : 1;
         }
-        if (a.cmd == "cameras") {  // host-only: camera matrices as the C-ABI receives them
+        if (a.cmd == "cameras") {  // host-only: the camera matrices the C-ABI receives (uint32 bit patterns)
             for (const char* n : {"config1", "orbit"}) {
                 const Camera c = preset_camera(n, W, H);
-                print_mat((std::string(n) + "_view_inv").c_str(), c.matrices.view.inverse().colmajor());
-                print_mat((std::string(n) + "_proj_inv").c_str(), c.matrices.perspective.inverse().colmajor());
+                print_mat(std::string(n) + "_view_inv", gm::inverse(c.matrices.view));
+                print_mat(std::string(n) + "_proj_inv", gm::inverse(c.matrices.perspective));
             }
-            Camera e;
-            e.setPosition({0.5, -1.0, 2.0});
-            e.setRotation({10.0, 20.0, 30.0});
-            print_mat("euler_view", e.matrices.view.colmajor());
-            if (a.has("transforms")) {
-                CameraLoader l;
-                std::string err;
-                if (!l.loadNerfCameraData(a.get("transforms"), &err)) throw std::runtime_error(err);
-                for (size_t i = 0; i < l.views.size(); ++i)
-                    print_mat(("nerf_w2c_" + std::to_string(i)).c_str(), l.views[i].colmajor());
+            Camera e;  // camera.hpp Euler camera, as VulkanFullRT drives it
+            e.setPerspective(FOV_Y, (float)W / H, NEAR_PLANE, FAR_PLANE);
+            e.setPosition(parse_vec3(a.get("position", "0.5,-1,2")));
+            e.setRotation(parse_vec3(a.get("rotation", "10,20,30")));
+            print_mat("euler_view", e.matrices.view);
+            print_mat("euler_view_inv", gm::inverse(e.matrices.view));
+            print_mat("euler_proj_inv", gm::inverse(e.matrices.perspective));
+            if (a.has("transforms")) {  // EVAL_QUALITY sequence: loadDatasetCamera + setDatasetCamera
+                Camera c;
+                c.setNearFar(NEAR_PLANE, FAR_PLANE);
+                c.loadDatasetCamera(nerf, a.get("transforms"), W, H);
+                for (uint32_t i = 0; i < c.getCamNames().size(); ++i) {
+                    c.setDatasetCamera(c.dataType, i, (float)W / H);
+                    print_mat("nerf_w2c_" + std::to_string(i), c.matrices.view);
+                    print_mat("nerf_view_inv_" + std::to_string(i), gm::inverse(c.matrices.view));
+                    print_mat("nerf_proj_inv_" + std::to_string(i), gm::inverse(c.matrices.perspective));
+                }
+            }
+            if (a.has("ply")) {  // light-field ring rig of the scene (calculateGaussianLightFieldSamples)
+                vk3DGRT::SplatSet s;
+                if (!vk3DGRT::PLYLoader().loadPLYModel(a.get("ply").c_str(), s)) throw std::runtime_error("cannot load ply");
+                std::vector<gm::mat4> vi;
+                gm::mat4 pi;
+                gvrt_host::lightfield_ring_rig(s, 4, W, H, vi, pi);
+                for (size_t i = 0; i < vi.size(); ++i) print_mat("ring_view_inv_" + std::to_string(i), vi[i]);
+                print_mat("ring_proj_inv", pi);
             }
             return 0;
         }
@@ -139,7 +153,7 @@ int main(int argc, char** argv) {
         const uint64_t m = app.prepare(ply, nullptr, &ap);
         const gvrt_stats st = app.stats();
         std::printf("prepared: %zu Gaussians, %llu after the enclosing pass; enclose %.3f ms, accel %.3f ms\n",
-                    app.splats.size(), (unsigned long long)m, st.enclose_ms, st.accel_ms);
+                    app.gModel.splatSet.size(), (unsigned long long)m, st.enclose_ms, st.accel_ms);
         ::mkdir(out.c_str(), 0755);
         const Camera cam = preset_camera(a.get("camera", "orbit"), W, H);
         if (a.cmd == "render") {
@@ -151,20 +165,21 @@ int main(int argc, char** argv) {
             const size_t n = app.evalCapture(a.get("transforms"), out, W, H);
             std::printf("wrote %zu views to %s\n", n, out.c_str());
         } else if (a.cmd == "lightfield") {
-            const size_t n = app.computeGaussianLightField(out, W, H);
+            app.gaussianLightField.sampleImageWidth = W;
+            app.gaussianLightField.sampleImageHeight = H;
+            const size_t n = app.computeGaussianLightField(out);
             std::printf("wrote %zu views + rayDirs.bin to %s\n", n, out.c_str());
         } else if (a.cmd == "hitcounts") {
             app.printRayHitCounts(cam, W, H, out + "/rayHitCountsOutput.txt");
             std::printf("wrote %s/rayHitCountsOutput.txt\n", out.c_str());
-        } else if (a.cmd == "bench") {
-            Benchmark b;
-            b.duration = std::atof(a.get("duration", "10").c_str());
-            b.warmup = std::atof(a.get("warmup", "1").c_str());
+        } else if (a.cmd == "bench") {  // vks::Benchmark (seconds are whole, as benchmark.hpp's uint32_t)
+            vks::Benchmark& b = app.benchmark;
+            b.duration = (uint32_t)std::atoi(a.get("duration", "10").c_str());
+            b.warmup = (uint32_t)std::atoi(a.get("warmup", "1").c_str());
             b.outputFrameTimes = a.has("frametimes");
             b.filename = out + "/fps.txt";
-            const double fps = app.benchmark(cam, W, H, b);
+            app.runBenchmark(cam, W, H);
             b.saveResults();
-            std::printf("frames : %zu\nfps    : %.2f\n", b.frameTimes.size(), fps);
         } else {
             return usage();
         }

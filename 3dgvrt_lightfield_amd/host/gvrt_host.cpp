@@ -1,5 +1,5 @@
 // gvrt_host.cpp — implementation of the C++ host layer (gvrt_host.h).  Reference file:line per class
-// in the header; the Python mirror (camera.py, app.py) follows the same formulas.
+// in the header; the Python mirror (camera.py, app.py) follows the same float32 formulas.
 #include "gvrt_host.h"
 
 #include <hip/hip_runtime_api.h>
@@ -7,191 +7,29 @@
 #include <algorithm>
 #include <cctype>
 #include <cfloat>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
-#include <limits>
+#include <iomanip>
+#include <iostream>
 #include <map>
-#include <memory>
+#include <numeric>
 #include <sstream>
 #include <stdexcept>
 #include <sys/stat.h>
 
-namespace gvrt_host {
+namespace {
 
-static void check(gvrt_status s, gvrt_handle h, const char* what) {
+void check(gvrt_status s, gvrt_handle h, const char* what) {
     if (s != GVRT_OK) throw std::runtime_error(std::string(what) + ": " + gvrt_last_error(h));
 }
 
-static void make_dir(const std::string& d) { ::mkdir(d.c_str(), 0755); }
+void make_dir(const std::string& d) { ::mkdir(d.c_str(), 0755); }
 
-// ------------------------------------------------------------------------------------------- math
-mat4 mat4::identity() {
-    mat4 r{};
-    for (int i = 0; i < 4; ++i) r.m[i][i] = 1.0;
-    return r;
-}
+}  // namespace
 
-mat4 mat4::operator*(const mat4& b) const {
-    mat4 r{};
-    for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j)
-            for (int k = 0; k < 4; ++k) r.m[i][j] += m[i][k] * b.m[k][j];
-    return r;
-}
-
-mat4 mat4::inverse() const {
-    double a[4][8];
-    for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 8; ++j) a[i][j] = j < 4 ? m[i][j] : (j - 4 == i ? 1.0 : 0.0);
-    for (int c = 0; c < 4; ++c) {
-        int p = c;
-        for (int r = c + 1; r < 4; ++r)
-            if (std::fabs(a[r][c]) > std::fabs(a[p][c])) p = r;
-        if (a[p][c] == 0.0) throw std::runtime_error("singular matrix");
-        if (p != c)
-            for (int j = 0; j < 8; ++j) std::swap(a[p][j], a[c][j]);
-        const double d = a[c][c];
-        for (int j = 0; j < 8; ++j) a[c][j] /= d;
-        for (int r = 0; r < 4; ++r) {
-            if (r == c) continue;
-            const double f = a[r][c];
-            if (f != 0.0)
-                for (int j = 0; j < 8; ++j) a[r][j] -= f * a[c][j];
-        }
-    }
-    mat4 r{};
-    for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j) r.m[i][j] = a[i][4 + j];
-    return r;
-}
-
-std::array<float, 16> mat4::colmajor() const {
-    std::array<float, 16> o{};
-    for (int c = 0; c < 4; ++c)
-        for (int r = 0; r < 4; ++r) o[4 * c + r] = (float)m[r][c];
-    return o;
-}
-
-static vec3 sub(const vec3& a, const vec3& b) { return {a[0] - b[0], a[1] - b[1], a[2] - b[2]}; }
-static vec3 add(const vec3& a, const vec3& b) { return {a[0] + b[0], a[1] + b[1], a[2] + b[2]}; }
-static vec3 scale(const vec3& a, double s) { return {a[0] * s, a[1] * s, a[2] * s}; }
-static double dot(const vec3& a, const vec3& b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-static vec3 cross(const vec3& a, const vec3& b) {
-    return {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
-}
-static vec3 normalize(const vec3& a) { return scale(a, 1.0 / std::sqrt(dot(a, a))); }
-
-// glm::lookAtRH
-mat4 look_at(const vec3& eye, const vec3& center, const vec3& up) {
-    const vec3 f = normalize(sub(center, eye));
-    const vec3 s = normalize(cross(f, up));
-    const vec3 u = cross(s, f);
-    mat4 m = mat4::identity();
-    for (int i = 0; i < 3; ++i) {
-        m.m[0][i] = s[i];
-        m.m[1][i] = u[i];
-        m.m[2][i] = -f[i];
-    }
-    m.m[0][3] = -dot(s, eye);
-    m.m[1][3] = -dot(u, eye);
-    m.m[2][3] = dot(f, eye);
-    return m;
-}
-
-// matrix_transform.inl:276-290 (Result[1][1] = -1/tan: image row 0 is the top)
-mat4 perspective_vulkan_no_depth_reverse(double fovy_rad, double aspect, double znear, double zfar) {
-    const double t = std::tan(fovy_rad / 2.0);
-    mat4 m{};
-    m.m[0][0] = 1.0 / (aspect * t);
-    m.m[1][1] = -1.0 / t;
-    m.m[3][2] = -1.0;
-    m.m[2][2] = -zfar / (zfar - znear);
-    m.m[2][3] = -(zfar * znear) / (zfar - znear);
-    return m;
-}
-
-// ------------------------------------------------------------------------------------------- model
-gvrt_splats SplatSet::view() const {
-    gvrt_splats s{};
-    s.n = size();
-    s.positions = positions.data();
-    s.f_dc = f_dc.data();
-    s.f_rest = f_rest.data();
-    s.opacity = opacity.data();
-    s.scale = scale.data();
-    s.rotation = rotation.data();
-    return s;
-}
-
-bool PLYLoader::loadPLYModel(const std::string& filename, SplatSet& out, std::string* err) {
-    gvrt_splat_buffers b{};
-    if (gvrt_ply_load(filename.c_str(), &b) != GVRT_OK) {
-        if (err) *err = gvrt_last_error(nullptr);
-        return false;
-    }
-    const size_t n = b.n;
-    auto take = [n](const float* p, size_t k) { return std::vector<float>(p, p + n * k); };
-    out.positions = take(b.positions, 3);
-    out.f_dc = take(b.f_dc, 3);
-    out.f_rest = take(b.f_rest, 45);
-    out.opacity = take(b.opacity, 1);
-    out.scale = take(b.scale, 3);
-    out.rotation = take(b.rotation, 4);
-    gvrt_ply_free(&b);
-    return true;
-}
-
-// ------------------------------------------------------------------------------------------- camera
-// camera.hpp rotateAxis: rotate (u, v) about u and rebuild n
-static void rotate_axis(double rad, vec3& u, vec3& v, vec3& n) {
-    const double s = std::sin(rad), c = std::cos(rad);
-    v = normalize(add(scale(v, c), scale(cross(u, v), s)));
-    n = normalize(cross(u, v));
-}
-
-void Camera::updateViewMatrix() {  // camera.hpp:31-58, N_IS_UP
-    vec3 u{1, 0, 0}, v{0, 0, 1}, n{0, -1, 0};
-    const double d2r = M_PI / 180.0;
-    if (rotation[1] * d2r != 0) rotate_axis(rotation[1] * d2r, v, n, u);
-    if (rotation[0] * d2r != 0) rotate_axis(rotation[0] * d2r, u, v, n);
-    if (rotation[2] * d2r != 0) rotate_axis(rotation[2] * d2r, n, u, v);
-    mat4 rt = mat4::identity();  // transpose of glm::mat4(vec4(u), vec4(v), vec4(n), ...)
-    for (int i = 0; i < 3; ++i) {
-        rt.m[0][i] = u[i];
-        rt.m[1][i] = v[i];
-        rt.m[2][i] = n[i];
-    }
-    mat4 tr = mat4::identity();
-    for (int i = 0; i < 3; ++i) tr.m[i][3] = -position[i];
-    matrices.view = rt * tr;  // glm::translate(transpose(rot), -position)
-}
-
-void Camera::setPosition(const vec3& p) {
-    position = p;
-    updateViewMatrix();
-}
-
-void Camera::setRotation(const vec3& r) {
-    rotation = r;
-    updateViewMatrix();
-}
-
-void Camera::setPerspective(double fov_deg, double aspect, double zn, double zf) {  // camera.hpp:157-182
-    fov = fov_deg;
-    znear = zn;
-    zfar = zf;
-    matrices.perspective = perspective_vulkan_no_depth_reverse(fov_deg * M_PI / 180.0, aspect, zn, zf);
-}
-
-void Camera::setLookAt(const vec3& eye, const vec3& target, const vec3& up) {
-    position = eye;
-    matrices.view = look_at(eye, target, up);
-}
-
-// ------------------------------------------------------------------------------------------- JSON
-// A minimal JSON reader for transforms_*.json (objects, arrays, numbers, strings, literals).
 namespace {
 struct JVal {
     enum Kind { NUL, NUM, STR, ARR, OBJ, BOOL } kind = NUL;
@@ -307,56 +145,317 @@ struct JParser {
 };
 }  // namespace
 
-// LoadCamera.hpp:57-85 (loadNerfCameraData) and :124-147 (c2wTow2cRT): w2c = [R^T | -R^T t]
-bool CameraLoader::loadNerfCameraData(const std::string& path, std::string* err) {
-    try {
-        std::ifstream f(path);
-        if (!f) throw std::runtime_error("cannot open " + path);
-        std::stringstream ss;
-        ss << f.rdbuf();
-        const std::string txt = ss.str();
-        JParser p(txt);
-        const JVal root = p.value();
-        if (root.kind != JVal::OBJ) throw std::runtime_error("transforms: not an object");
-        auto it = root.obj.find("camera_angle_x");
-        camera_angle_x = it != root.obj.end() ? it->second.num : 0.0;
-        auto fr = root.obj.find("frames");
-        if (fr == root.obj.end() || fr->second.kind != JVal::ARR) throw std::runtime_error("transforms: no frames");
-        views.clear();
-        for (const JVal& frame : fr->second.arr) {
-            auto tm = frame.obj.find("transform_matrix");
-            if (tm == frame.obj.end() || tm->second.arr.size() < 3) throw std::runtime_error("frame without transform_matrix");
-            mat4 c2w = mat4::identity();
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 4; ++c) c2w.m[r][c] = tm->second.arr[r].arr.at(c).num;
-            mat4 w2c = mat4::identity();
-            for (int r = 0; r < 3; ++r) {
-                for (int c = 0; c < 3; ++c) w2c.m[r][c] = c2w.m[c][r];
-                w2c.m[r][3] = -(c2w.m[0][r] * c2w.m[0][3] + c2w.m[1][r] * c2w.m[1][3] + c2w.m[2][r] * c2w.m[2][3]);
-            }
-            views.push_back(w2c);
-        }
-        return true;
-    } catch (const std::exception& e) {
-        if (err) *err = e.what();
+// ================================================================================== gvrt_host::Device
+namespace gvrt_host {
+Device::Device(int ord) : ordinal(ord) {
+    if (gvrt_get_device_properties(ord, &properties) != GVRT_OK)
+        throw std::runtime_error(std::string("gvrt_get_device_properties: ") + gvrt_last_error(nullptr));
+}
+}  // namespace gvrt_host
+
+// ================================================================================== vk3DGRT
+namespace vk3DGRT {
+
+bool PLYLoader::loadPLYModel(const char* filename, SplatSet& output) {
+    gvrt_splat_buffers b{};
+    if (gvrt_ply_load(filename, &b) != GVRT_OK) {
+        std::fprintf(stderr, "PLYLoader: %s\n", gvrt_last_error(nullptr));
         return false;
+    }
+    const size_t n = b.n;
+    auto take = [n](const float* p, size_t k) { return std::vector<float>(p, p + n * k); };
+    output.positions = take(b.positions, 3);
+    output.f_dc = take(b.f_dc, 3);
+    output.f_rest = take(b.f_rest, 45);
+    output.opacity = take(b.opacity, 1);
+    output.scale = take(b.scale, 3);
+    output.rotation = take(b.rotation, 4);
+    gvrt_ply_free(&b);
+    return true;
+}
+
+void Model::load3DGRTModel(std::string filename, gvrt_host::Device* /*device*/) {
+    const size_t dot = filename.find_last_of('.');
+    if (dot == std::string::npos) throw std::runtime_error("Extension not found");
+    const std::string ext = filename.substr(dot + 1);
+    if (ext != "ply") throw std::runtime_error("Unsupported Extensnion: \"" + ext);
+    PLYLoader plyLoader;
+    if (!plyLoader.loadPLYModel(filename.c_str(), splatSet)) throw std::runtime_error("cannot load " + filename);
+}
+
+void Model::allocateAttributeBuffers(gvrt_host::Device* /*device*/, gvrt_host::Queue queue) {
+    const int n = (int)splatSet.size();
+    vertices.count = 3 * 12 * n;
+    indices.count = 3 * 20 * n;
+    positions.count = 3 * n;
+    rotations.count = 4 * n;
+    scales.count = 3 * n;
+    densities.count = n;
+    featuresAlbedo.count = 3 * n;
+    featuresSpecular.count = 45 * n;  // SPECULAR_DIMENSION (Define.h:132-133)
+    gvrt_splats s{};
+    s.n = splatSet.size();
+    s.positions = splatSet.positions.data();
+    s.f_dc = splatSet.f_dc.data();
+    s.f_rest = splatSet.f_rest.data();
+    s.opacity = splatSet.opacity.data();
+    s.scale = splatSet.scale.data();
+    s.rotation = splatSet.rotation.data();
+    check(gvrt_load_splats(queue, &s), queue, "gvrt_load_splats");
+    gvrt_device_buffers b{};
+    check(gvrt_get_device_buffers(queue, &b), queue, "gvrt_get_device_buffers");
+    auto bind = [](Attributes& a, const void* p) { a.storageBuffer = {p, sizeof(float) * (uint64_t)a.count}; };
+    bind(positions, b.positions);
+    bind(rotations, b.rotations);
+    bind(scales, b.scales);
+    bind(densities, b.densities);
+    bind(featuresAlbedo, b.features_albedo);
+    bind(featuresSpecular, b.features_specular);
+    vertices.storageBuffer = {};
+    indices.storageBuffer = {};
+}
+
+void Model::attachEnclosingBuffers(gvrt_host::Queue queue) {
+    gvrt_device_buffers b{};
+    check(gvrt_get_device_buffers(queue, &b), queue, "gvrt_get_device_buffers");
+    // the proxy soup of the survivors (saveIdx order); the reference sizes it for all N (Q4)
+    vertices.storageBuffer = {b.vertices, b.vertices ? 144 * b.m : 0};
+    indices.storageBuffer = {b.indices, b.indices ? 240 * b.m : 0};
+}
+
+}  // namespace vk3DGRT
+
+// ================================================================================== CameraLoader
+void CameraLoader::calcIntrinsics(float cameraAngleX, uint32_t width, uint32_t height, float, float) {
+    float fx, fy;
+    fx = fy = 0.5f * width / std::tan(0.5f * cameraAngleX);
+    (void)fx;
+    fovy = 2 * std::atan(height / (2 * fy));
+    fovy *= 57.2957795131;  // RAD2DEGREE (LoadCamera.hpp:20), a double
+}
+
+void CameraLoader::c2wTow2cRT(CameraFrame& frame) {
+    const gm::mat3 R = gm::mat3_of(frame.transformMatrix);
+    const gm::vec3 T(frame.transformMatrix[3].x, frame.transformMatrix[3].y, frame.transformMatrix[3].z);
+    const gm::mat3 R_inv = gm::transpose(R);
+    const gm::vec3 T_inv = -R_inv * T;
+    frame.transformMatrix = gm::mat4(R_inv);
+    frame.transformMatrix[3] = gm::vec4(T_inv, 1.0f);
+    nerfCameras.centers.push_back(T_inv);
+    frame.position = -gm::vec3(frame.transformMatrix[3].x, frame.transformMatrix[3].y, frame.transformMatrix[3].z);
+    gm::vec3 scale;
+    scale.x = gm::length(gm::vec3(frame.transformMatrix[0].x, frame.transformMatrix[0].y, frame.transformMatrix[0].z));
+    scale.y = gm::length(gm::vec3(frame.transformMatrix[1].x, frame.transformMatrix[1].y, frame.transformMatrix[1].z));
+    scale.z = gm::length(gm::vec3(frame.transformMatrix[2].x, frame.transformMatrix[2].y, frame.transformMatrix[2].z));
+    gm::mat3 rot;
+    for (int i = 0; i < 3; ++i)
+        rot[i] = gm::vec3(frame.transformMatrix[i].x, frame.transformMatrix[i].y, frame.transformMatrix[i].z) / scale[i];
+    frame.rotation = gm::quat_cast(rot);
+}
+
+void CameraLoader::loadNerfCameraData(const std::string& jsonPath, uint32_t width, uint32_t height, float znear,
+                                      float zfar) {
+    std::ifstream fin(jsonPath);
+    if (!fin.is_open()) throw std::runtime_error("Failed to open file : " + jsonPath);
+    std::stringstream ss;
+    ss << fin.rdbuf();
+    const std::string txt = ss.str();
+    JParser p(txt);
+    const JVal j = p.value();
+    if (j.kind != JVal::OBJ) throw std::runtime_error("transforms: not an object");
+    auto ang = j.obj.find("camera_angle_x");
+    if (ang == j.obj.end()) throw std::runtime_error("transforms: no camera_angle_x");
+    nerfCameras.cameraAngleX = (float)ang->second.num;  // get<float>()
+    calcIntrinsics(nerfCameras.cameraAngleX, width, height, znear, zfar);
+    auto fr = j.obj.find("frames");
+    if (fr == j.obj.end() || fr->second.kind != JVal::ARR) throw std::runtime_error("transforms: no frames");
+    int i = 0;
+    for (const JVal& frame : fr->second.arr) {
+        CameraFrame f;
+        auto fp = frame.obj.find("file_path");
+        if (fp != frame.obj.end()) f.filePath = fp->second.str;
+        auto tm = frame.obj.find("transform_matrix");
+        if (tm == frame.obj.end() || tm->second.arr.size() != 4) throw std::runtime_error("frame without transform_matrix");
+        for (int row = 0; row < 4; ++row)
+            for (int col = 0; col < 4; ++col) f.transformMatrix[col][row] = (float)tm->second.arr[row].arr.at(col).num;
+        c2wTow2cRT(f);
+        nerfCameras.frames.push_back(f);
+        camNames.push_back(std::to_string(i));
+        i++;
     }
 }
 
-// ------------------------------------------------------------------------------------------- benchmark
-bool Benchmark::saveResults() const {  // benchmark.hpp:77-104
-    FILE* f = std::fopen(filename.c_str(), "w");
-    if (!f) return false;
-    const size_t n = frameTimes.size();
-    std::fprintf(f, "device,driverversion,duration (ms),frames,fps\n");
-    std::fprintf(f, "%s,%s,%.4f,%zu,%.4f\n", device.c_str(), driver.c_str(), runtime, n, n / (runtime / 1000.0));
-    if (outputFrameTimes) {
-        std::fprintf(f, "\nframe,ms\n");
-        for (size_t i = 0; i < n; ++i) std::fprintf(f, "%zu,%.4f\n", i, frameTimes[i]);
+void CameraLoader::PrintCameraData(const NerfCameraData& data) {
+    std::cout << "camera_angle_x: " << data.cameraAngleX << "\n";
+    for (const auto& frame : data.frames) {
+        std::cout << "File: " << frame.filePath << "\nMatrix:\n";
+        std::cout << "transform matrix : \n";
+        for (int i = 0; i < 4; ++i)
+            std::cout << frame.transformMatrix[0][i] << " " << frame.transformMatrix[1][i] << " "
+                      << frame.transformMatrix[2][i] << " " << frame.transformMatrix[3][i] << "\n";
+        std::cout << "-----\n";
     }
-    std::fclose(f);
-    return true;
 }
+
+// ================================================================================== Camera
+void Camera::updateViewMatrix() {  // camera.hpp:31-58 (N_IS_UP)
+    const gm::mat4 currentMatrix = matrices.view;
+    gm::vec3 uVec(1.0f, 0.0f, 0.0f), vVec(0.0f, 0.0f, 1.0f), nVec(0.0f, -1.0f, 0.0f);
+    if (gm::radians(rotation.y) != 0) rotateAxis(gm::radians(rotation.y), &vVec, &nVec, &uVec);
+    if (gm::radians(rotation.x) != 0) rotateAxis(gm::radians(rotation.x), &uVec, &vVec, &nVec);
+    if (gm::radians(rotation.z) != 0) rotateAxis(gm::radians(rotation.z), &nVec, &uVec, &vVec);
+    const gm::mat4 rot(gm::vec4(uVec, 0.0f), gm::vec4(vVec, 0.0f), gm::vec4(nVec, 0.0f), gm::vec4(0.0f, 0.0f, 0.0f, 1.0f));
+    matrices.view = gm::translate(gm::transpose(rot), -position);
+    if (matrices.view != currentMatrix) updated = true;
+}
+
+void Camera::rotateAxis(float rad_angle, gm::vec3* u, gm::vec3* v, gm::vec3* n) {  // camera.hpp:124-141
+    const float sina = std::sin(rad_angle), cosa = std::cos(rad_angle);
+    *v = gm::normalize(*v * cosa + gm::cross(*u, *v) * sina);
+    *n = gm::normalize(gm::cross(*u, *v));
+}
+
+void Camera::setNearFar(float _znear, float _zfar) {
+    znear = _znear;
+    zfar = _zfar;
+}
+
+void Camera::setNerfCamera(uint32_t idx) {
+    if (idx >= cameraLoader.nerfCameras.frames.size()) throw std::runtime_error("NeRF camera index out of range");
+    matrices.view = cameraLoader.nerfCameras.frames[idx].transformMatrix;
+}
+
+void Camera::setDatasetCamera(DatasetType t, uint32_t idx, float aspect) {  // camera.hpp:106-113
+    if (t == nerf) {
+        setPerspective(cameraLoader.fovy, aspect, znear, zfar);
+        setPerspective(FOV_Y, aspect, znear, zfar);
+        setNerfCamera(idx);
+    }
+}
+
+void Camera::loadDatasetCamera(DatasetType t, std::string path, uint32_t width, uint32_t height) {
+    if (t == nerf) cameraLoader.loadNerfCameraData(path, width, height, znear, zfar);
+    dataType = t;
+}
+
+void Camera::setPerspective(float fov_, float aspect, float znear_, float zfar_) {  // camera.hpp:157-182
+    const gm::mat4 currentMatrix = matrices.perspective;
+    fov = fov_;
+    znear = znear_;
+    zfar = zfar_;
+    matrices.perspective = gm::perspective_Vulkan_no_depth_reverse(gm::radians(fov_), aspect, znear_, zfar_);
+    if (matrices.view != currentMatrix) updated = true;  // (sic: the reference compares the view)
+}
+
+void Camera::updateAspectRatio(float aspect) {
+    const gm::mat4 currentMatrix = matrices.perspective;
+    matrices.perspective = gm::perspective_Vulkan_no_depth_reverse(gm::radians(fov), aspect, znear, zfar);
+    if (matrices.view != currentMatrix) updated = true;
+}
+
+void Camera::setPosition(gm::vec3 p) {
+    position = p;
+    updateViewMatrix();
+}
+
+void Camera::setRotation(gm::vec3 r) {
+    rotation = r;
+    updateViewMatrix();
+}
+
+void Camera::rotate(gm::vec3 delta) {
+    rotation += delta;
+    updateViewMatrix();
+}
+
+void Camera::setTranslation(gm::vec3 t) {
+    position = t;
+    updateViewMatrix();
+}
+
+void Camera::translate(gm::vec3 delta) {
+    position += delta;
+    updateViewMatrix();
+}
+
+void Camera::update(float deltaTime) {  // camera.hpp:229-281
+    updated = false;
+    if ((type == CameraType::firstperson || type == CameraType::SG_camera) && moving()) {
+        const float moveSpeed = deltaTime * movementSpeed;
+        gm::vec3 uVec(1.0f, 0.0f, 0.0f), vVec(0.0f, 0.0f, 1.0f), nVec(0.0f, -1.0f, 0.0f);
+        if (gm::radians(rotation.y) != 0) rotateAxis(gm::radians(rotation.y), &vVec, &nVec, &uVec);
+        if (gm::radians(rotation.x) != 0) rotateAxis(gm::radians(rotation.x), &uVec, &vVec, &nVec);
+        if (gm::radians(rotation.z) != 0) rotateAxis(gm::radians(rotation.z), &nVec, &uVec, &vVec);
+        if (keys.forward) position -= nVec * moveSpeed;
+        if (keys.backward) position += nVec * moveSpeed;
+        if (keys.left) position -= uVec * moveSpeed;
+        if (keys.right) position += uVec * moveSpeed;
+        if (keys.up) position += vVec * moveSpeed;
+        if (keys.down) position -= vVec * moveSpeed;
+    }
+    updateViewMatrix();  // !LOAD_NERF_CAMERA (Define.h:24)
+}
+
+void Camera::setLookAt(const gm::vec3& eye, const gm::vec3& target, const gm::vec3& up) {
+    position = eye;
+    matrices.view = gm::lookAt(eye, target, up);
+}
+
+// ================================================================================== vks::Benchmark
+namespace vks {
+
+void Benchmark::run(std::function<void()> renderFunc, gvrt_device_properties props) {  // benchmark.hpp:37-75
+    active = true;
+    deviceProps = props;
+    std::cout << std::fixed << std::setprecision(3);
+    {
+        double tMeasured = 0.0;
+        while (tMeasured < (warmup * 1000)) {
+            auto tStart = std::chrono::high_resolution_clock::now();
+            renderFunc();
+            tMeasured += std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - tStart).count();
+        }
+    }
+    while (runtime < (duration * 1000.0)) {
+        auto tStart = std::chrono::high_resolution_clock::now();
+        renderFunc();
+        auto tDiff = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - tStart).count();
+        runtime += tDiff;
+        frameTimes.push_back(tDiff);
+        frameCount++;
+        if (outputFrames != -1 && outputFrames == (int)frameCount) break;
+    }
+    std::cout << "Benchmark finished" << "\n";
+    std::cout << "device : " << deviceProps.device_name << " (driver version: " << deviceProps.driver_version << ")" << "\n";
+    std::cout << "runtime: " << (runtime / 1000.0) << "\n";
+    std::cout << "frames : " << frameCount << "\n";
+    std::cout << "fps    : " << frameCount / (runtime / 1000.0) << "\n";
+}
+
+void Benchmark::saveResults() {  // benchmark.hpp:77-104
+    std::ofstream result(filename, std::ios::out);
+    if (!result.is_open()) return;
+    result << std::fixed << std::setprecision(4);
+    result << "device,driverversion,duration (ms),frames,fps" << "\n";
+    result << deviceProps.device_name << "," << deviceProps.driver_version << "," << runtime << "," << frameCount << ","
+           << frameCount / (runtime / 1000.0) << "\n";
+    if (outputFrameTimes && !frameTimes.empty()) {
+        result << "\n" << "frame,ms" << "\n";
+        for (size_t i = 0; i < frameTimes.size(); i++) result << i << "," << frameTimes[i] << "\n";
+        const double tMin = *std::min_element(frameTimes.begin(), frameTimes.end());
+        const double tMax = *std::max_element(frameTimes.begin(), frameTimes.end());
+        const double tAvg = std::accumulate(frameTimes.begin(), frameTimes.end(), 0.0) / (double)frameTimes.size();
+        std::cout << "best   : " << (1000.0 / tMin) << " fps (" << tMin << " ms)" << "\n";
+        std::cout << "worst  : " << (1000.0 / tMax) << " fps (" << tMax << " ms)" << "\n";
+        std::cout << "avg    : " << (1000.0 / tAvg) << " fps (" << tAvg << " ms)" << "\n";
+        std::cout << "\n";
+    }
+    result.flush();
+}
+
+}  // namespace vks
+
+namespace gvrt_host {
 
 // ------------------------------------------------------------------------------------------- PNG
 static uint32_t crc32_update(uint32_t crc, const uint8_t* p, size_t n) {
@@ -436,9 +535,58 @@ bool write_png(const std::string& path, const uint8_t* rgba, uint32_t w, uint32_
     return ok;
 }
 
-// ------------------------------------------------------------------------------------------- app
-GvrtApp::GvrtApp(int device) : device_(device) {
-    check(gvrt_create(device, &h_), nullptr, "gvrt_create");
+
+// ================================================================================== presets, rig
+gm::vec3 orbit_eye(float radius, float elevation_deg, float azimuth_deg) {
+    const float el = gm::radians(elevation_deg), az = gm::radians(azimuth_deg);
+    const float ce = std::cos(el);
+    return gm::vec3(radius * ce * std::sin(az), radius * std::sin(el), radius * ce * std::cos(az));
+}
+
+Camera preset_camera(const std::string& name, uint32_t w, uint32_t h) {
+    Camera c;
+    const float aspect = (float)w / (float)h;
+    if (name == "config1") {
+        c.setLookAt(gm::vec3(0.0f, 0.0f, 3.0f), gm::vec3(), gm::vec3(0.0f, 1.0f, 0.0f));
+        c.setPerspective(FOV_Y, aspect, NEAR_PLANE, FAR_PLANE);
+    } else {
+        c.setLookAt(orbit_eye(4.0f, 20.0f, 30.0f), gm::vec3(), gm::vec3(0.0f, 1.0f, 0.0f));
+        c.setPerspective(50.0f, aspect, NEAR_PLANE, FAR_PLANE);
+    }
+    return c;
+}
+
+void lightfield_ring_rig(const vk3DGRT::SplatSet& s, uint32_t ncams, uint32_t width, uint32_t height,
+                         std::vector<gm::mat4>& view_inv, gm::mat4& proj_inv) {
+    float minX, minY, minZ, maxX, maxY, maxZ;  // VulkanFullRT.cpp:1527-1544 (max starts at FLT_MIN, Q15)
+    minX = minY = minZ = FLT_MAX;
+    maxX = maxY = maxZ = FLT_MIN;
+    for (size_t i = 0; i < s.size(); i++) {
+        const float x = s.positions[i * 3], y = s.positions[i * 3 + 1], z = s.positions[i * 3 + 2];
+        if (x < minX) minX = x;
+        if (y < minY) minY = y;
+        if (z < minZ) minZ = z;
+        if (x > maxX) maxX = x;
+        if (y > maxY) maxY = y;
+        if (z > maxZ) maxZ = z;
+    }
+    const gm::vec3 center((minX + maxX) / 2, (minY + maxY) / 2, (minZ + maxZ) / 2);
+    const float maxR = std::max(std::max(maxX - minX, maxY - minY), maxZ - minZ) / 2;
+    const gm::vec3 up(0, 0, 1);
+    const gm::vec3 cameraPos[4] = {gm::vec3(center.x + maxR, center.y, center.z),
+                                   gm::vec3(center.x, center.y + maxR, center.z),
+                                   gm::vec3(center.x - maxR, center.y, center.z),
+                                   gm::vec3(center.x, center.y - maxR, center.z)};
+    view_inv.clear();
+    for (uint32_t i = 0; i < ncams; i++) view_inv.push_back(gm::inverse(gm::lookAt(cameraPos[i % 4], center, up)));
+    // 135 degree fov, aspect (float)(width / height) with integer division (Q15), :1596 / :1604
+    proj_inv = gm::inverse(gm::perspective_Vulkan_no_depth_reverse(gm::radians(135.0f), (float)(width / height),
+                                                                   NEAR_PLANE, FAR_PLANE));
+}
+
+// ================================================================================== GvrtApp
+GvrtApp::GvrtApp(int dev) : device(dev) {
+    check(gvrt_create(dev, &h_), nullptr, "gvrt_create");
     gvrt_default_render_params(&params);
 }
 
@@ -447,78 +595,63 @@ GvrtApp::~GvrtApp() {
 }
 
 uint64_t GvrtApp::prepare(const std::string& ply, const gvrt_enclosing_params* ep, const gvrt_accel_params* ap) {
-    std::string err;
-    if (!PLYLoader().loadPLYModel(ply, splats, &err)) throw std::runtime_error("cannot load " + ply + ": " + err);
-    const gvrt_splats s = splats.view();
-    check(gvrt_load_splats(h_, &s), h_, "gvrt_load_splats");
+    gModel.load3DGRTModel(ply, &device);
+    gModel.allocateAttributeBuffers(&device, h_);
     gvrt_enclosing_params e;
     gvrt_default_enclosing_params(&e);
     uint64_t m = 0;
     check(gvrt_build_enclosing(h_, ep ? ep : &e, &m), h_, "gvrt_build_enclosing");
+    gModel.attachEnclosingBuffers(h_);
     if (ap) check(gvrt_build_accel_ex(h_, ap), h_, "gvrt_build_accel_ex");
     else check(gvrt_build_accel(h_), h_, "gvrt_build_accel");
     return m;
 }
 
-void GvrtApp::draw(const Camera& cam, uint32_t width, uint32_t height, uint8_t* rgba8, uint32_t* hit_counts) {
-    const auto vi = cam.matrices.view.inverse().colmajor();
-    const auto pi = cam.matrices.perspective.inverse().colmajor();
+void GvrtApp::updateUniformBuffer(const Camera& cam) {
+    uniformDataDynamic.viewInverse = gm::inverse(cam.matrices.view);
+    uniformDataDynamic.projInverse = gm::inverse(cam.matrices.perspective);
+}
+
+void GvrtApp::draw(uint32_t width, uint32_t height, uint8_t* rgba8, uint32_t* hit_counts) {
     gvrt_image img{rgba8, nullptr, nullptr, hit_counts, 0, 0};
-    check(gvrt_render(h_, &params, vi.data(), pi.data(), width, height, 1, nullptr, 0, &img), h_, "gvrt_render");
+    check(gvrt_render(h_, &params, uniformDataDynamic.viewInverse.data(), uniformDataDynamic.projInverse.data(), width,
+                      height, 1, nullptr, 0, &img),
+          h_, "gvrt_render");
+}
+
+void GvrtApp::draw(const Camera& cam, uint32_t width, uint32_t height, uint8_t* rgba8, uint32_t* hit_counts) {
+    updateUniformBuffer(cam);
+    draw(width, height, rgba8, hit_counts);
 }
 
 size_t GvrtApp::evalCapture(const std::string& transforms, const std::string& out_dir, uint32_t width,
                             uint32_t height) {
-    CameraLoader loader;
-    std::string err;
-    if (!loader.loadNerfCameraData(transforms, &err)) throw std::runtime_error(err);
+    camera.setNearFar(NEAR_PLANE, FAR_PLANE);
+    camera.loadDatasetCamera(nerf, transforms, width, height);
     make_dir(out_dir);
-    Camera cam;
-    cam.setPerspective(FOV_Y, (double)width / height, NEAR_PLANE, FAR_PLANE);  // setDatasetCamera's FOV_Y
     std::vector<uint8_t> frame((size_t)4 * width * height);
-    for (size_t i = 0; i < loader.views.size(); ++i) {
-        cam.matrices.view = loader.views[i];  // camera.setNerfCamera: w2c is the view matrix
-        draw(cam, width, height, frame.data());
+    const size_t nviews = camera.getCamNames().size();
+    for (uint32_t i = 0; i < nviews; ++i) {
+        camera.setDatasetCamera(camera.dataType, i, (float)width / height);  // VulkanFullRT.cpp:2154
+        draw(camera, width, height, frame.data());
         if (!write_png(out_dir + "/r_" + std::to_string(i) + ".png", frame.data(), width, height))
             throw std::runtime_error("cannot write " + out_dir);
     }
-    return loader.views.size();
+    return nviews;
 }
 
-void lightfield_ring_rig(const SplatSet& s, uint32_t ncams, uint32_t width, uint32_t height,
-                         std::vector<float>& view_inv, std::array<float, 16>& proj_inv) {
-    // bbox of the raw positions with max initialised to FLT_MIN (Q15)
-    float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {FLT_MIN, FLT_MIN, FLT_MIN};
-    for (size_t i = 0; i < s.size(); ++i)
-        for (int k = 0; k < 3; ++k) {
-            mn[k] = std::min(mn[k], s.positions[3 * i + k]);
-            mx[k] = std::max(mx[k], s.positions[3 * i + k]);
-        }
-    vec3 center;
-    float maxr = 0.0f;
-    for (int k = 0; k < 3; ++k) {
-        center[k] = (double)((mn[k] + mx[k]) / 2.0f);
-        maxr = std::max(maxr, mx[k] - mn[k]);
-    }
-    const double r = (double)maxr / 2.0;
-    const vec3 cams[4] = {add(center, {r, 0, 0}), add(center, {0, r, 0}), sub(center, {r, 0, 0}), sub(center, {0, r, 0})};
-    view_inv.clear();
-    for (uint32_t i = 0; i < ncams; ++i) {
-        const auto v = look_at(cams[i % 4], center, {0.0, 0.0, 1.0}).inverse().colmajor();
-        view_inv.insert(view_inv.end(), v.begin(), v.end());
-    }
-    // 135 degree fov, aspect (float)(width / height) with integer division (Q15)
-    proj_inv = perspective_vulkan_no_depth_reverse(135.0 * M_PI / 180.0, (double)(float)(width / height), NEAR_PLANE,
-                                                   FAR_PLANE)
-                   .inverse()
-                   .colmajor();
+void GvrtApp::calculateGaussianLightFieldSamples() {
+    lightfield_ring_rig(gModel.splatSet, gaussianLightField.samplingCameraNum, gaussianLightField.sampleImageWidth,
+                        gaussianLightField.sampleImageHeight, gaussianLightField.viewInverse,
+                        gaussianLightField.projInverse);
 }
 
-size_t GvrtApp::computeGaussianLightField(const std::string& out_dir, uint32_t width, uint32_t height) {
-    const uint32_t ncams = 4;  // VulkanFullRT.cpp:169-171
+size_t GvrtApp::computeGaussianLightField(const std::string& out_dir) {
+    calculateGaussianLightFieldSamples();
+    const uint32_t ncams = gaussianLightField.samplingCameraNum;
+    const uint32_t width = gaussianLightField.sampleImageWidth, height = gaussianLightField.sampleImageHeight;
     std::vector<float> vi;
-    std::array<float, 16> pi;
-    lightfield_ring_rig(splats, ncams, width, height, vi, pi);
+    for (const gm::mat4& m : gaussianLightField.viewInverse) vi.insert(vi.end(), m.data(), m.data() + 16);
     gvrt_render_params p = params;  // the light-field raygen: pixel centre, alpha starts at 1
     p.pixel_offset = 0.5f;
     p.alpha_init = 1.0f;
@@ -526,7 +659,8 @@ size_t GvrtApp::computeGaussianLightField(const std::string& out_dir, uint32_t w
     std::vector<uint8_t> rgba((size_t)4 * width * height * ncams);
     std::vector<float> dirs((size_t)4 * width * height * ncams);
     gvrt_image img{rgba.data(), nullptr, dirs.data(), nullptr, 0, 0};
-    check(gvrt_render(h_, &p, vi.data(), pi.data(), width, height, ncams, nullptr, 0, &img), h_, "gvrt_render");
+    check(gvrt_render(h_, &p, vi.data(), gaussianLightField.projInverse.data(), width, height, ncams, nullptr, 0, &img),
+          h_, "gvrt_render");
     make_dir(out_dir);
     for (uint32_t c = 0; c < ncams; ++c)
         if (!write_png(out_dir + "/view_" + std::to_string(c) + ".png", rgba.data() + (size_t)4 * width * height * c,
@@ -551,32 +685,27 @@ void GvrtApp::printRayHitCounts(const Camera& cam, uint32_t width, uint32_t heig
     std::fclose(f);
 }
 
-double GvrtApp::benchmark(const Camera& cam, uint32_t width, uint32_t height, Benchmark& b) {
+double GvrtApp::runBenchmark(const Camera& cam, uint32_t width, uint32_t height) {
+    // frames go to device memory (the reference renders into its swapchain image; no readback)
     void* frame = nullptr;
-    if (hipSetDevice(device_) != hipSuccess || hipMalloc(&frame, (size_t)4 * width * height) != hipSuccess)
+    if (hipSetDevice(device.ordinal) != hipSuccess || hipMalloc(&frame, (size_t)4 * width * height) != hipSuccess)
         throw std::runtime_error("device frame allocation failed");
-    hipDeviceProp_t prop{};
-    if (hipGetDeviceProperties(&prop, device_) == hipSuccess) {
-        b.device = prop.name;
-        std::replace(b.device.begin(), b.device.end(), ',', ' ');
-    }
-    int drv = 0;
-    if (hipDriverGetVersion(&drv) == hipSuccess) b.driver = std::to_string(drv);
-    const auto vi = cam.matrices.view.inverse().colmajor();
-    const auto pi = cam.matrices.perspective.inverse().colmajor();
+    updateUniformBuffer(cam);
     gvrt_image img{frame, nullptr, nullptr, nullptr, 1, 0};
-    double fps = 0.0;
     try {
-        fps = b.run([&] {  // one frame = render + wait, as the reference's frame with its fence
-            check(gvrt_render(h_, &params, vi.data(), pi.data(), width, height, 1, nullptr, 0, &img), h_,
-                  "gvrt_render");
-        });
+        benchmark.run(
+            [&] {  // one frame = render + wait, as the reference's frame with its fence
+                check(gvrt_render(h_, &params, uniformDataDynamic.viewInverse.data(),
+                                  uniformDataDynamic.projInverse.data(), width, height, 1, nullptr, 0, &img),
+                      h_, "gvrt_render");
+            },
+            device.properties);
     } catch (...) {
         (void)hipFree(frame);
         throw;
     }
     (void)hipFree(frame);
-    return fps;
+    return benchmark.frameCount / (benchmark.runtime / 1000.0);
 }
 
 gvrt_stats GvrtApp::stats() const {

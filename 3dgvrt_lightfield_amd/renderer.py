@@ -197,6 +197,8 @@ class Renderer:
         p = params if params is not None else self.render_params(**kw)
         vi = np.ascontiguousarray(view_inv, np.float32).reshape(-1)
         pi = np.ascontiguousarray(proj_inv, np.float32).reshape(16)
+        if vi.size != 16 * ncams or pi.size != 16:
+            raise ValueError("view_inv must hold 16*ncams floats and proj_inv 16")
         t, nt = self.tile_array(tiles)
         img = _lib.Image(rgba8_ptr, rgba32f_ptr, ray_dirs_ptr, hit_counts_ptr, 1, 1 if packed else 0)
         fn = lib().gvrt_render_async if async_ else lib().gvrt_render
@@ -207,9 +209,25 @@ class Renderer:
         """gvrt_sync: wait for the frames queued by render_device(async_=True); render_ms() is then their mean."""
         check(lib().gvrt_sync(self.h), self.h)
 
-    def unpack_tiles_rgba8(self, packed_ptr, tiles, width, height, frame_ptr):
+    def unpack_tiles_rgba8(self, packed_ptr, tiles, width, height, frame_ptr, ncams=1):
+        """gvrt_unpack_tiles_rgba8: tile-packed rgba8 (device) -> frame [ncams][H][W][4] (device)."""
         t, nt = self.tile_array(tiles)
-        check(lib().gvrt_unpack_tiles_rgba8(self.h, packed_ptr, _lib.vptr(t), nt, width, height, frame_ptr), self.h)
+        check(lib().gvrt_unpack_tiles_rgba8(self.h, packed_ptr, _lib.vptr(t), nt, width, height, ncams, frame_ptr),
+              self.h)
+
+    def device_buffers(self):
+        """gvrt_get_device_buffers: device pointers of Model::Attributes and the enclosing outputs."""
+        b = _lib.DeviceBuffers()
+        check(lib().gvrt_get_device_buffers(self.h, C.byref(b)), self.h)
+        return {k: getattr(b, k) for k, _ in b._fields_}
+
+
+def device_properties(device=0):
+    """gvrt_get_device_properties: name, driver version, CUs, memory, arch of a HIP device."""
+    p = _lib.DeviceProperties()
+    check(lib().gvrt_get_device_properties(int(device), C.byref(p)))
+    return {"device_name": p.device_name.decode(), "driver_version": p.driver_version,
+            "compute_units": p.compute_units, "total_memory": p.total_memory, "arch_name": p.arch_name.decode()}
 
 
 def device_count():

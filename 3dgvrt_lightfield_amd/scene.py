@@ -59,7 +59,7 @@ def config1(n=10_000, seed=CONFIG1_SEED):
 
 def config1_camera(width=256, height=256):
     """eye (0,0,3) -> origin, up +y, fovy 39.6 deg (Define.h:33-35)."""
-    return cam.pinhole((0.0, 0.0, 3.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), cam.FOV_Y, width / height)
+    return cam.pinhole((0.0, 0.0, 3.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), cam.FOV_Y, cam.aspect_ratio(width, height))
 
 
 def mipnerf_standin(n=1_000_000, seed=1):
@@ -89,7 +89,7 @@ def mipnerf_standin(n=1_000_000, seed=1):
 
 def mipnerf_camera(width=1920, height=1080, azimuth_deg=30.0):
     """Orbit camera radius 4, elevation 20 deg, fovy 50 deg."""
-    return cam.orbit_camera(4.0, 20.0, azimuth_deg, (0.0, 0.0, 0.0), 50.0, width / height)
+    return cam.orbit_camera(4.0, 20.0, azimuth_deg, (0.0, 0.0, 0.0), 50.0, cam.aspect_ratio(width, height))
 
 
 CONFIGS = {

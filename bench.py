@@ -84,19 +84,14 @@ def main():
 
     # cameras: an N-view planar rig around the config-2 orbit camera (view 0 = the config camera)
     if args.config == "config1":
-        vi0, pi = gv.scene.config1_camera(W, H)
-        eye = np.array([0.0, 0.0, 3.0])
-        target = np.zeros(3)
-        fovy = gv.camera.FOV_Y
+        eye, fovy = (0.0, 0.0, 3.0), gv.camera.FOV_Y
     else:
-        el, az = math.radians(20.0), math.radians(30.0)
-        eye = np.array([4 * math.cos(el) * math.sin(az), 4 * math.sin(el), 4 * math.cos(el) * math.cos(az)])
-        target = np.zeros(3)
-        fovy = 50.0
+        eye, fovy = gv.camera.orbit_eye(4.0, 20.0, 30.0), 50.0  # = scene.mipnerf_camera (view 0)
+    target = (0.0, 0.0, 0.0)
     views = world if args.split == "views" else 1
     views = max(views, ncams_cfg if args.config == "lightfield" else 1)
     vis, pi = gv.camera.lightfield_grid_rig(eye, target, (0.0, 1.0, 0.0), nx=views, ny=1, spacing=0.1,
-                                            fovy_deg=fovy, aspect=W / H)
+                                            fovy_deg=fovy, aspect=gv.camera.aspect_ratio(W, H))
     vis = vis.reshape(views, 16)
     if args.split == "views":
         my_views = [v for v in range(views) if v % world == rank]

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define GVRT_ABI_VERSION 1
+#define GVRT_ABI_VERSION 2
 
 typedef int32_t gvrt_status;
 #define GVRT_OK 0
@@ -196,13 +196,47 @@ gvrt_status gvrt_render_async(gvrt_handle h, const gvrt_render_params* p, const 
                               const gvrt_image* out);
 gvrt_status gvrt_sync(gvrt_handle h);
 
+/* Device identity for the benchmark report: the VkPhysicalDeviceProperties fields vks::Benchmark
+ * prints and writes to fps.txt (deviceName, driverVersion; base/benchmark.hpp:23,67-70,85). */
+typedef struct {
+    char device_name[256];
+    uint32_t driver_version;  /* hipDriverGetVersion */
+    uint32_t compute_units;
+    uint64_t total_memory;    /* bytes of device memory */
+    char arch_name[64];       /* e.g. "gfx950:sramecc+:xnack-" */
+} gvrt_device_properties;
+gvrt_status gvrt_get_device_properties(int device, gvrt_device_properties* out);
+
+/* Device buffers held by a handle, i.e. vk3DGRT::Model::Attributes::storageBuffer
+ * (base/Vulkan3DGRTModel.h:43-48, filled by allocateAttributeBuffers, Vulkan3DGRTModel.cpp:163-222)
+ * and the Gaussian Enclosing outputs bound to the render pass (ParticleDensity / SH storage buffers,
+ * VulkanFullRT.cpp:1045-1062).  Device pointers, valid until the next load / build / destroy on the
+ * handle; NULL where the stage has not run (vertices / indices also need emit_triangles). */
+typedef struct {
+    uint64_t n;                       /* splats loaded */
+    const float* positions;           /* 3n  */
+    const float* rotations;           /* 4n  */
+    const float* scales;              /* 3n  */
+    const float* densities;           /* n   raw opacity */
+    const float* features_albedo;     /* 3n  f_dc */
+    const float* features_specular;   /* 45n f_rest (coefficient-major) */
+    uint64_t m;                       /* survivors of the enclosing pass */
+    const float* vertices;            /* 36m proxy vertices */
+    const uint32_t* indices;          /* 60m proxy triangle indices */
+    const float* particle_density;    /* 12m std140 ParticleDensity records */
+    const float* particle_sph;        /* 48m SH records */
+} gvrt_device_buffers;
+gvrt_status gvrt_get_device_buffers(gvrt_handle h, gvrt_device_buffers* out);
+
 /* Enable per-render statistics (crossings/accepted/rounds; costs one atomic per wave). */
 gvrt_status gvrt_set_stats(gvrt_handle h, int enable);
 gvrt_status gvrt_get_stats(gvrt_handle h, gvrt_stats* s);
 
-/* Scatter a tile-packed rgba8 buffer (gathered from ranks) into a full frame; device ptrs. */
+/* Scatter a tile-packed rgba8 buffer (gathered from ranks) into a full frame [ncams][H][W][4]; device
+ * ptrs.  Every tile must lie inside the frame (tx < ceil(W/8), ty < ceil(H/8), cam < ncams), else
+ * GVRT_ERR_INVALID_ARG and nothing is written. */
 gvrt_status gvrt_unpack_tiles_rgba8(gvrt_handle h, const void* packed, const gvrt_tile* tiles,
-                                    uint64_t ntiles, uint32_t width, uint32_t height,
+                                    uint64_t ntiles, uint32_t width, uint32_t height, uint32_t ncams,
                                     void* frame);
 
 /* --------------------------------------------------------------------------------------- */

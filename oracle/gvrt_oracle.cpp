@@ -237,7 +237,7 @@ struct RayState {
 };
 
 bool processHit(const Scene& s, V3 o, V3 d, uint32_t idx, float minKernelDensity, float minAlpha,
-                uint32_t sphEvalDegree, RayState& st) {
+                uint32_t sphEvalDegree, RayState& st, HitEval* eval = nullptr) {
     const float* rec = s.density + 12ull * idx;
     const V3 pos = v3(rec[0], rec[1], rec[2]);
     const float dens = rec[3];
@@ -255,6 +255,7 @@ bool processHit(const Scene& s, V3 o, V3 d, uint32_t idx, float minKernelDensity
     const float gres = particleResponse(grayDist);
     const float galpha = std::min(0.99f, gres * dens);
     const bool acceptHit = (gres > minKernelDensity) && (galpha > minAlpha);
+    if (eval) *eval = HitEval{gres, galpha};
     if (acceptHit) {
         const float weight = galpha * st.T;
         const V3 grds = scl * grd * dot(grd, -1.0f * gro);
@@ -553,8 +554,24 @@ struct Hit {
     float t;
 };
 
+// debugging aid: when set (single-threaded trace of one ray), every processed crossing is appended as
+// {id, t, gres, galpha, T after, accepted, round}
+static thread_local std::vector<float>* g_trace = nullptr;
+
 // The per-ray ray-march: particleRendering.comp:117-191 (RQ) / raygen.rgen:303-383 (RT).
 // out_stats[3*r] = processed crossings (X_r), [3r+1] = accepted (A_r), [3r+2] = rounds.
+// out_margin[3*r .. 3*r+2] (optional; parity accounting, not part of the reference algorithm): how
+// close the ray came to a decision that a few-ulp different float evaluation (GPU exp / rsqrt / rcp,
+// FMA contraction) could take the other way.
+//   [0] relative distance to a threshold: |gres/hitMin - 1| and |galpha/alphaMin - 1| of every processed
+//       crossing, |T/minTransmittance - 1| after every accepted one;
+//   [1] relative t gap |t_i - t_j| / |t_i| between consecutive accepted crossings (their composite
+//       order);
+//   [2] relative t gap at a boundary: the first crossing of a round (if accepted) against the last one of
+//       the round before, the last slot of a full buffer against the nearest crossing left out, the
+//       crossing that ends the ray (T <= minTransmittance) against its successor, a ray grazing a proxy
+//       whose crossings would be accepted (relative chord |tout - tin| / |t|), and 0 for a crossing
+//       dropped because its t tied bitwise with `last` (the exclusive-tmin round boundary, Q13).
 struct OracleScene {
     Scene s;
     Bvh bvh;
@@ -620,7 +637,8 @@ void oracle_scene_destroy(void* h) { delete static_cast<OracleScene*>(h); }
 
 int oracle_scene_render(void* h, const oracle_params* P, const float* viewInverse, const float* projInverse,
                         uint32_t W, uint32_t H, uint32_t ncams, const uint64_t* subset, uint64_t nsubset,
-                        float* out_rgba, float* out_depth, float* out_ray_dirs, uint32_t* out_stats, int nthreads) {
+                        float* out_rgba, float* out_depth, float* out_ray_dirs, uint32_t* out_stats,
+                        float* out_margin, int nthreads) {
     OracleScene* os = static_cast<OracleScene*>(h);
     if (!os || !P || !viewInverse || !projInverse || !out_rgba) return -1;
     if (P->proxy_mode != os->proxy_mode) return -2;
@@ -661,6 +679,10 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
         intersectAABB(P->aabb, o, d, tminb, tmaxb);
         float last = std::max(0.0f, tminb - EPS_T);
         Hit kb[MAX_HIT_PER_TRACE];
+        float m_thr = INFINITY, m_t = INFINITY, m_b = INFINITY, prev_t = NAN, prev_acc_t = NAN;
+        bool round_start = false;
+        uint32_t prev_id = INVALID_PARTICLE_ID;
+        std::vector<uint32_t> last_ids;  // ids processed with t == last (tie detection, out_margin)
         std::vector<uint32_t> stack;
         stack.reserve(128);
         while (last <= tmaxb && st.T > P->min_transmittance) {
@@ -668,10 +690,16 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
             ++rounds;
             const float tmin = last + EPS_T, tmax = tmaxb + EPS_T;
             for (uint32_t i = 0; i < MAX_HIT_PER_TRACE; ++i) kb[i] = Hit{INVALID_PARTICLE_ID, INFINITE_DISTANCE};
+            float t_out = INFINITE_DISTANCE;
             // ---- trace(): driver traversal + any-hit (anyhit.rahit:40-71)
             auto anyhit = [&](uint32_t pid, float t) {
                 const bool inRange = (P->tmin_inclusive ? t >= tmin : t > tmin) && t <= tmax;
-                if (!inRange) return;
+                if (!inRange) {
+                    if (out_margin && t == last && t <= tmax &&
+                        std::find(last_ids.begin(), last_ids.end(), pid) == last_ids.end())
+                        m_b = 0.0f;  // dropped only because its t ties with the last processed crossing
+                    return;
+                }
                 if (P->drop_rejected) {
                     const HitEval he = evalResponse(s, pid, o, d);
                     if (!(he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min)) return;
@@ -682,6 +710,8 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                         if (hit.t < kb[i].t) std::swap(hit, kb[i]);
                     }
                 }
+                // out_margin: the nearest crossing left out of (or pushed out of) the full buffer
+                if (hit.id != INVALID_PARTICLE_ID) t_out = std::min(t_out, hit.t);
             };
             stack.clear();
             stack.push_back(0);
@@ -712,7 +742,15 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                     const uint32_t g = bvh.items[nd.left + k];
                     if (P->proxy_mode == 1) {
                         float tin, tout;
-                        if (icosaCross(s, g, o, d, tin, tout)) {
+                        const bool crossed = icosaCross(s, g, o, d, tin, tout);
+                        if (out_margin && std::fabs(tout - tin) < 1e-5f * std::max(std::fabs(tin), std::fabs(tout))) {
+                            // grazing the proxy: whether it is crossed at all is a few-ulp decision; it
+                            // matters when its crossings would be composited
+                            const HitEval he = evalResponse(s, g, o, d);
+                            if (he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min)
+                                m_b = std::min(m_b, std::fabs(tout - tin) / std::max(std::fabs(tin), 1e-30f));
+                        }
+                        if (crossed) {
                             anyhit(g, tin);
                             anyhit(g, tout);
                         }
@@ -739,12 +777,45 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                 }
             }
             if (kb[0].id == INVALID_PARTICLE_ID) break;
+            auto gap = [](float a, float b) { return std::fabs(a - b) / std::max(std::fabs(a), 1e-30f); };
+            // out_margin: a crossing tied with the buffer's last slot may or may not make this round,
+            // depending on arrival order
+            if (out_margin && kb[MAX_HIT_PER_TRACE - 1].id != INVALID_PARTICLE_ID && t_out < INFINITE_DISTANCE)
+                m_b = std::min(m_b, gap(kb[MAX_HIT_PER_TRACE - 1].t, t_out));
+            round_start = true;
             // ---- process k hits
             for (uint32_t i = 0; i < MAX_HIT_PER_TRACE; ++i) {
                 const Hit h = kb[i];
                 if (h.id != INVALID_PARTICLE_ID && st.T > P->min_transmittance) {
+                    HitEval ev{0.0f, 0.0f};
                     const bool acc = processHit(s, o, d, h.id, P->hit_min_gaussian_response, P->alpha_min,
-                                                P->sph_eval_degree, st);
+                                                P->sph_eval_degree, st, &ev);
+                    if (g_trace)
+                        g_trace->insert(g_trace->end(), {(float)h.id, h.t, ev.gres, ev.galpha, st.T, acc ? 1.0f : 0.0f,
+                                                         (float)rounds});
+                    if (out_margin) {
+                        m_thr = std::min(m_thr, std::fabs(ev.gres / P->hit_min_gaussian_response - 1.0f));
+                        m_thr = std::min(m_thr, std::fabs(ev.galpha / P->alpha_min - 1.0f));
+                        if (acc) m_thr = std::min(m_thr, std::fabs(st.T / P->min_transmittance - 1.0f));
+                        // (an inclusive tmin re-finds the same crossing: not an ordering question)
+                        const bool refound = h.id == prev_id && h.t == prev_t;
+                        if (acc && round_start && prev_t == prev_t && !refound) m_b = std::min(m_b, gap(h.t, prev_t));
+                        if (acc && prev_acc_t == prev_acc_t && !refound) m_t = std::min(m_t, gap(h.t, prev_acc_t));
+                        round_start = false;
+                        prev_t = h.t;
+                        prev_id = h.id;
+                        if (acc) prev_acc_t = h.t;
+                        if (h.t > last) last_ids.clear();
+                        if (h.t >= last) last_ids.push_back(h.id);
+                        // the crossing that ends the ray against its successor: a tie decides which of
+                        // the two is composited
+                        if (acc && !(st.T > P->min_transmittance)) {
+                            const float tn = i + 1 < MAX_HIT_PER_TRACE && kb[i + 1].id != INVALID_PARTICLE_ID
+                                                 ? kb[i + 1].t
+                                                 : t_out;
+                            if (tn < INFINITE_DISTANCE) m_b = std::min(m_b, gap(h.t, tn));
+                        }
+                    }
                     last = std::max(last, h.t);
                     ++nproc;
                     nacc += acc ? 1 : 0;
@@ -759,6 +830,11 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
             out_stats[3 * oi + 1] = nacc;
             out_stats[3 * oi + 2] = rounds;
         }
+        if (out_margin) {
+            out_margin[3 * oi] = m_thr;
+            out_margin[3 * oi + 1] = m_t;
+            out_margin[3 * oi + 2] = m_b;
+        }
     }
     return 0;
 }
@@ -767,15 +843,30 @@ int oracle_render(const float* verts, const uint32_t* tris, const float* density
                   uint32_t M, const oracle_params* P, const float* viewInverse,
                   const float* projInverse, uint32_t W, uint32_t H, uint32_t ncams,
                   const uint64_t* subset, uint64_t nsubset, float* out_rgba, float* out_depth,
-                  float* out_ray_dirs, uint32_t* out_stats, int nthreads) {
+                  float* out_ray_dirs, uint32_t* out_stats, float* out_margin, int nthreads) {
     if (!P) return -1;
     void* h = oracle_scene_create(verts, tris, density, sh, M, P->proxy_mode, P->kernel_min_response,
                                   P->kernel_opts, P->kernel_degree);
     if (!h) return -1;
     const int rc = oracle_scene_render(h, P, viewInverse, projInverse, W, H, ncams, subset, nsubset, out_rgba,
-                                       out_depth, out_ray_dirs, out_stats, nthreads);
+                                       out_depth, out_ray_dirs, out_stats, out_margin, nthreads);
     oracle_scene_destroy(h);
     return rc;
+}
+
+// Processed-crossing trace of one ray (debugging): 7 floats per crossing (see g_trace); returns the count.
+int oracle_scene_trace(void* h, const oracle_params* P, const float* viewInverse, const float* projInverse,
+                       uint32_t W, uint32_t H, uint32_t ncams, uint64_t ray, float* out, int maxn) {
+    std::vector<float> tr;
+    g_trace = &tr;
+    float rgba[4];
+    const int rc = oracle_scene_render(h, P, viewInverse, projInverse, W, H, ncams, &ray, 1, rgba, nullptr, nullptr,
+                                       nullptr, nullptr, 1);
+    g_trace = nullptr;
+    if (rc) return rc;
+    const int n = (int)(tr.size() / 7);
+    std::memcpy(out, tr.data(), sizeof(float) * 7 * std::min(n, maxn));
+    return n;
 }
 
 // Single-Gaussian response helper for known-answer tests.

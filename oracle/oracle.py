@@ -40,14 +40,17 @@ def lib():
         L.oracle_enclose.argtypes = [vp] * 6 + [C.c_uint32, C.c_float, C.c_uint32, C.c_float] + [vp] * 6
         L.oracle_enclose.restype = C.c_int
         L.oracle_render.argtypes = [vp, vp, vp, vp, C.c_uint32, C.POINTER(OracleParams), vp, vp, C.c_uint32,
-                                    C.c_uint32, C.c_uint32, vp, C.c_uint64, vp, vp, vp, vp, C.c_int]
+                                    C.c_uint32, C.c_uint32, vp, C.c_uint64, vp, vp, vp, vp, vp, C.c_int]
         L.oracle_render.restype = C.c_int
         L.oracle_scene_create.argtypes = [vp, vp, vp, vp, C.c_uint32, C.c_uint32, C.c_float, C.c_uint32, C.c_float]
         L.oracle_scene_create.restype = vp
         L.oracle_scene_destroy.argtypes = [vp]
         L.oracle_scene_render.argtypes = [vp, C.POINTER(OracleParams), vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp,
-                                          C.c_uint64, vp, vp, vp, vp, C.c_int]
+                                          C.c_uint64, vp, vp, vp, vp, vp, C.c_int]
         L.oracle_scene_render.restype = C.c_int
+        L.oracle_scene_trace.argtypes = [vp, C.POINTER(OracleParams), vp, vp, C.c_uint32, C.c_uint32, C.c_uint32,
+                                         C.c_uint64, vp, C.c_int]
+        L.oracle_scene_trace.restype = C.c_int
         L.oracle_eval_response.argtypes = [vp] * 5
         L.oracle_kernel_scale.argtypes = [C.c_float, C.c_float, C.c_uint32, C.c_float]
         L.oracle_kernel_scale.restype = C.c_float
@@ -116,18 +119,20 @@ def render(enc, view_inv, proj_inv, width, height, ncams=1, params=None, subset=
     rgba = np.zeros((nr, 4), np.float32)
     depth = np.zeros(nr, np.float32)
     stats = np.zeros((nr, 3), np.uint32)
+    margin = np.zeros((nr, 3), np.float32)
     dirs = np.zeros((nr if subset is not None else width * height * ncams, 4), np.float32) if ray_dirs else None
     rc = lib().oracle_render(_p(enc["verts"]), _p(enc["tris"]), _p(enc["density"]), _p(enc["sh"]), enc["m"],
                              C.byref(p), _p(vi), _p(pi), width, height, ncams, _p(sub), 0 if sub is None else len(sub),
-                             _p(rgba), _p(depth), _p(dirs), _p(stats), int(threads))
+                             _p(rgba), _p(depth), _p(dirs), _p(stats), _p(margin), int(threads))
     assert rc == 0
-    out = {"rgba32f": rgba, "depth": depth, "stats": stats}
+    out = {"rgba32f": rgba, "depth": depth, "stats": stats, "margin": margin}
     if ray_dirs:
         out["ray_dirs"] = dirs
     if subset is None:
         out["rgba32f"] = rgba.reshape(ncams, height, width, 4)
         out["stats"] = stats.reshape(ncams, height, width, 3)
         out["depth"] = depth.reshape(ncams, height, width)
+        out["margin"] = margin.reshape(ncams, height, width, 3)
     return out
 
 
@@ -173,7 +178,7 @@ class Scene:
     def __del__(self):
         self.close()
 
-    def render(self, view_inv, proj_inv, width, height, ncams=1, subset=None, threads=0, **kw):
+    def render(self, view_inv, proj_inv, width, height, ncams=1, subset=None, threads=0, margin=False, **kw):
         p = default_params(proxy_mode=self.proxy_mode, **self.kw, **kw)
         vi = np.ascontiguousarray(view_inv, np.float32).reshape(-1)
         pi = np.ascontiguousarray(proj_inv, np.float32).reshape(16)
@@ -181,7 +186,41 @@ class Scene:
         sub = None if subset is None else np.ascontiguousarray(subset, np.uint64)
         rgba = np.zeros((nr, 4), np.float32)
         stats = np.zeros((nr, 3), np.uint32)
+        marg = np.zeros((nr, 3), np.float32) if margin else None
         rc = lib().oracle_scene_render(self.h, C.byref(p), _p(vi), _p(pi), width, height, ncams, _p(sub),
-                                       0 if sub is None else len(sub), _p(rgba), None, None, _p(stats), int(threads))
+                                       0 if sub is None else len(sub), _p(rgba), None, None, _p(stats), _p(marg),
+                                       int(threads))
         assert rc == 0, rc
-        return {"rgba32f": rgba, "stats": stats}
+        out = {"rgba32f": rgba, "stats": stats}
+        if margin:
+            out["margin"] = marg
+        return out
+
+
+    def trace(self, view_inv, proj_inv, width, height, ray, ncams=1, maxn=4096, **kw):
+        """Processed crossings of one ray (debugging): array of (id, t, gres, galpha, T after, accepted, round)."""
+        p = default_params(proxy_mode=self.proxy_mode, **self.kw, **kw)
+        vi = np.ascontiguousarray(view_inv, np.float32).reshape(-1)
+        pi = np.ascontiguousarray(proj_inv, np.float32).reshape(16)
+        out = np.zeros((maxn, 7), np.float32)
+        n = lib().oracle_scene_trace(self.h, C.byref(p), _p(vi), _p(pi), width, height, ncams, int(ray), _p(out), maxn)
+        assert n >= 0, n
+        return out[:min(n, maxn)]
+
+
+# Parity accounting (see out_margin in gvrt_oracle.cpp): a ray is "on a threshold" when one of its
+# composite decisions lies within THR_EPS (relative) of the hit / alpha / transmittance threshold, two
+# consecutive accepted crossings lie within PAIR_EPS in t, or a crossing at a round / buffer /
+# termination boundary lies within BOUND_EPS in t of its neighbour (or ties bitwise at the exclusive
+# tmin).  Only such rays may decide differently under a few-ulp different float evaluation (the GPU's
+# v_exp / v_rsq / v_rcp and FMA contraction; the t of a crossing is measured to differ by up to ~1e-6
+# relative); every other ray must match.
+THR_EPS = 1e-4
+PAIR_EPS = 2e-6
+BOUND_EPS = 1e-5
+
+
+def ambiguous(margin):
+    """Boolean mask of rays whose result legitimately depends on ulp-level float differences."""
+    m = np.asarray(margin, np.float32).reshape(-1, 3)
+    return (m[:, 0] < THR_EPS) | (m[:, 1] < PAIR_EPS) | (m[:, 2] < BOUND_EPS)

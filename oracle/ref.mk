@@ -7,7 +7,7 @@ CXX ?= g++
 INC = -I$(REF)/base -I$(REF)/external -I$(REF)/external/glm -I$(REF)/external/miniply -I$(REF)/external/vulkan
 FLAGS = -O2 -std=c++20 -ffunction-sections -fdata-sections -w
 
-all: _ref/ref_ply_dump
+all: _ref/ref_ply_dump _ref/ref_camera_dump
 
 _ref/%.o: | _ref
 _ref:
@@ -26,3 +26,10 @@ _ref/ref_ply_dump: _ref/ref_ply_dump.o _ref/Vulkan3DGRTModel.o _ref/miniply.o
 	$(CXX) -Wl,--gc-sections -o $@ $^
 
 .PHONY: all
+
+# The reference's camera math (base/camera.hpp, base/LoadCamera.hpp, vendored glm + nlohmann json),
+# with the reference's own glm defines (base/VulkanRTBase.h:51-53).  Plain -O2 for x86-64: SSE float
+# arithmetic, no FMA contraction, libm sinf/cosf/tanf -- the same arithmetic the host mirrors use.
+CAM_DEFS = -DGLM_FORCE_RADIANS -DGLM_FORCE_DEPTH_ZERO_TO_ONE -DGLM_ENABLE_EXPERIMENTAL
+_ref/ref_camera_dump: ref_camera_dump.cpp $(REF)/base/camera.hpp $(REF)/base/LoadCamera.hpp | _ref
+	$(CXX) -O2 -std=c++17 -ffp-contract=off -w $(CAM_DEFS) -I$(REF)/base -I$(REF)/external/glm -I$(REF)/external/tinygltf $< -o $@

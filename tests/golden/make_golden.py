@@ -3,7 +3,9 @@
 The reference itself cannot run here (GLSL + Vulkan RT, no SPIR-V compiler or Vulkan device; SURVEY
 §8c), so these vectors are the oracle's restatement on seeded inputs.  They pin the oracle against
 regressions; the oracle in turn is pinned by the analytic known-answer tests in
-tests/test_oracle_kat.py.  Run:  python tests/golden/make_golden.py
+tests/test_oracle_kat.py.  The camera matrices stored with them (view_inv / proj_inv) are the
+reference's own: camera.py is bit-identical to base/camera.hpp + vendored glm compiled from the
+reference sources (tests/test_camera_reference.py).  Run:  python tests/golden/make_golden.py
 """
 import importlib
 import os
@@ -33,7 +35,7 @@ def main():
         sh_head=e["sh"][: 48 * 256], verts_head=e["verts"][: 36 * 256], tris_head=e["tris"][: 60 * 256],
         view_inv=vi, proj_inv=pi,
         rgba_tri=tri["rgba32f"], stats_tri=tri["stats"], rgba_analytic=ana["rgba32f"], stats_analytic=ana["stats"],
-        rgba_rt=rt["rgba32f"])
+        margin_analytic=ana["margin"], rgba_rt=rt["rgba32f"])
     # light-field ring rig (raygenGaussianLightField.rgen), 4 x 24 x 24, rayDirs layout [cam][x][y]
     vl, pl = gv.camera.lightfield_ring_rig(s["positions"], 4, 24, 24)
     lf = O.render(e, vl, pl, 24, 24, ncams=4, proxy_mode=0, pixel_offset=0.5, alpha_init=1.0, ray_dirs=True,

@@ -33,7 +33,8 @@ def test_every_declared_symbol_is_exported(gv):
 
 STRUCTS = {"gvrt_splats": "Splats", "gvrt_enclosing_params": "EnclosingParams", "gvrt_render_params": "RenderParams",
            "gvrt_tile": "Tile", "gvrt_image": "Image", "gvrt_stats": "Stats", "gvrt_splat_buffers": "SplatBuffers",
-           "gvrt_accel_params": "AccelParams"}
+           "gvrt_accel_params": "AccelParams", "gvrt_device_properties": "DeviceProperties",
+           "gvrt_device_buffers": "DeviceBuffers"}
 
 
 def test_struct_layouts_match_header(gv):
@@ -80,6 +81,11 @@ def test_no_device_is_a_status_not_an_abort(gv):
     # NULL handles are rejected, never dereferenced
     assert gv.lib().gvrt_build_accel(None) == -1
     assert gv.lib().gvrt_render(None, None, None, None, 1, 1, 1, None, 0, None) == -1
+    from importlib import import_module
+    L = import_module("3dgvrt_lightfield_amd._lib")
+    props = L.DeviceProperties()
+    assert gv.lib().gvrt_get_device_properties(0, C.byref(props)) == -5
+    assert gv.lib().gvrt_get_device_buffers(None, C.byref(L.DeviceBuffers())) == -1
 
 
 def test_ply_roundtrip_and_reorder(gv, tmp_path):

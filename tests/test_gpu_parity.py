@@ -3,9 +3,16 @@
 Tolerances (north star: "pixel-for-pixel within a stated float tolerance", PSNR >= 50 dB):
   * enclosing records: rtol 2e-6 / atol 1e-7 (expf / 1/sqrt ulps; FMA contraction on gfx950)
   * survivor count and compaction order: exact
-  * render, float RGBA vs the oracle with the same analytic proxy: |d rgb| <= 2e-3 on >= 99.9 % of
-    pixels, max |d rgb| <= 0.05 (a crossing whose response sits on the 0.0113 threshold can flip),
-    accepted-hit count (alpha channel) equal on >= 99.9 % of pixels
+  * render, float RGBA vs the oracle with the same analytic proxy, per ray:
+      - rays "on a threshold" are accounted separately: the oracle reports, per ray, how close any of its
+        composite decisions came to a threshold (response vs hitMinGaussianResponse, alpha vs 1/255,
+        T vs minTransmittance: relative margin < 1e-4), how close two consecutive composited crossings
+        came in t (relative gap < 2e-6) and how close a crossing at a round / full-buffer / termination
+        boundary came to its neighbour (< 1e-5, or a bitwise tie dropped at the exclusive tmin, Q13),
+        see oracle.ambiguous.  Only these rays may legitimately decide differently under the GPU's
+        few-ulp exp / rsqrt / rcp; they must be rare (<= 2 %, ~1 % measured);
+      - every other ray: |d rgb| <= 1e-4 on >= 99.99 % of them, max |d rgb| <= 5e-3, and the accepted-hit
+        count (alpha channel) equal;
   * render vs the literal restatement (20-triangle soup, watertight triangle test): PSNR >= 50 dB
 """
 import os
@@ -19,15 +26,24 @@ RTOL, ATOL = 2e-6, 1e-7
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def _cmp_images(a, b, frac_tol=1e-3, max_tol=0.05, tol=2e-3):
+def _cmp_images(a, ref, margin=None, frac_tol=1e-4, tol=1e-4, max_tol=5e-3, amb_max=0.02):
+    """a: HIP rgba; ref: oracle output dict (rgba32f + margin) or a bare rgba array with `margin` given.
+    See the module docstring for the accounting."""
+    if isinstance(ref, dict):
+        margin = ref["margin"] if margin is None else margin
+        ref = ref["rgba32f"]
+    import oracle as O
     a = np.asarray(a, np.float64).reshape(-1, 4)
-    b = np.asarray(b, np.float64).reshape(-1, 4)
-    d = np.abs(a[:, :3] - b[:, :3]).max(axis=1)
-    bad = (d > tol).mean()
-    assert bad <= frac_tol, f"{bad:.5f} of pixels differ by more than {tol} (max {d.max():.4g})"
-    assert d.max() <= max_tol, f"max |d rgb| = {d.max():.4g}"
-    am = (a[:, 3] != b[:, 3]).mean()
-    assert am <= frac_tol, f"{am:.5f} of pixels have a different accepted-hit count"
+    b = np.asarray(ref, np.float64).reshape(-1, 4)
+    amb = O.ambiguous(margin) if margin is not None else np.zeros(len(a), bool)
+    assert amb.sum() <= max(amb_max * amb.size, 3), f"{int(amb.sum())} of {amb.size} rays on a threshold"
+    d = np.abs(a[:, :3] - b[:, :3]).max(axis=1)[~amb]
+    bad = (d > tol).mean() if d.size else 0.0
+    assert bad <= frac_tol, f"{bad:.6f} of off-threshold rays differ by more than {tol} (max {d.max():.4g})"
+    assert d.size == 0 or d.max() <= max_tol, f"max |d rgb| = {d.max():.4g} on an off-threshold ray"
+    am = (a[:, 3] != b[:, 3])[~amb]
+    assert am.sum() <= frac_tol * am.size, f"{int(am.sum())} off-threshold rays differ in accepted-hit count"
+    return int(amb.sum())
 
 
 # ------------------------------------------------------------------ enclosing pass
@@ -69,9 +85,10 @@ def test_render_config1_vs_oracle_analytic(renderer, gv, O, config1, config1_enc
     vi, pi = gv.scene.config1_camera(W, H)
     out = renderer.render(vi, pi, W, H, mode=mode, hit_counts=True)
     ref = O.render(config1_enc, vi, pi, W, H, proxy_mode=1)
-    _cmp_images(out["rgba32f"], ref["rgba32f"])
+    _cmp_images(out["rgba32f"], ref)
     hc = out["hit_counts"].reshape(-1)
-    assert (hc != ref["stats"].reshape(-1, 3)[:, 1]).mean() <= 1e-3
+    amb = O.ambiguous(ref["margin"])
+    assert (hc != ref["stats"].reshape(-1, 3)[:, 1])[~amb].sum() == 0
     # rgba8 is the quantised float image
     np.testing.assert_array_equal(out["rgba8"], gv.quantize_rgba8(out["rgba32f"]))
 
@@ -86,22 +103,34 @@ def test_render_config1_vs_literal_triangles_psnr(renderer, gv, O, config1, conf
     assert p >= 50.0, p
 
 
-def test_fast_equals_literal(renderer, gv, config1):
+def _fast_vs_literal(O, enc, fast, lit, vi, pi, W, H, tol=1e-4, **kw):
+    """FAST and LITERAL composite the same crossings in the same order through the same response function,
+    so they agree to float rounding on every ray except one the oracle flags as on a threshold or as a
+    bitwise t tie across a 16-hit round boundary (the reference's exclusive tmin drops the tied crossing in
+    LITERAL, FAST's rounds fall elsewhere).  Exact accounting: every differing ray is re-marched by the
+    oracle and must carry that flag."""
+    fa, fb = np.asarray(fast, np.float64).reshape(-1, 4), np.asarray(lit, np.float64).reshape(-1, 4)
+    d = np.abs(fa[:, :3] - fb[:, :3]).max(axis=1)
+    differ = np.nonzero((d > tol) | (fa[:, 3] != fb[:, 3]))[0]
+    if differ.size:
+        ref = O.render(enc, vi, pi, W, H, proxy_mode=1, subset=differ.astype(np.uint64), **kw)
+        flagged = O.ambiguous(ref["margin"])
+        assert flagged.all(), (f"{int((~flagged).sum())} rays differ between FAST and LITERAL without a tie or "
+                               f"threshold flag: {differ[~flagged][:10]}, |d| {d[differ[~flagged][:10]]}")
+    return int(differ.size)
+
+
+def test_fast_equals_literal(renderer, gv, O, config1, config1_enc):
     renderer.prepare(config1)
     W, H = 200, 120
     vi, pi = gv.scene.config1_camera(W, H)
     a = renderer.render(vi, pi, W, H, mode=gv.MODE_FAST)
     b = renderer.render(vi, pi, W, H, mode=gv.MODE_LITERAL)
-    # Same composited sequence, except (a) ulp-level FMA-contraction differences between the two
-    # instantiations and (b) a crossing whose t ties bitwise with the last crossing of a 16-hit round:
-    # the reference's exclusive tmin drops it (LITERAL reproduces that), FAST's rounds fall elsewhere.
-    fa, fb = a["rgba32f"].reshape(-1, 4), b["rgba32f"].reshape(-1, 4)
-    d = np.abs(fa[:, :3] - fb[:, :3]).max(axis=1)
-    assert (d > 1e-4).mean() <= 2e-4 and d.max() <= 0.05, (int((d > 1e-4).sum()), float(d.max()))
-    assert (fa[:, 3] != fb[:, 3]).mean() <= 2e-4
+    n = _fast_vs_literal(O, config1_enc, a["rgba32f"], b["rgba32f"], vi, pi, W, H)
+    assert n <= 1e-3 * W * H
 
 
-def test_fast_skips_the_empty_trailing_round(renderer, gv, config1):
+def test_fast_skips_the_empty_trailing_round(renderer, gv, O, config1, config1_enc):
     """A FAST k-buffer that did not fill held every admitted crossing, so the round the reference would
     trace next (and find empty) is skipped: on the sparse config-1 scene most rays leave it unterminated,
     and each of them costs LITERAL (the reference's loop) one more, empty round than FAST; the images
@@ -118,9 +147,7 @@ def test_fast_skips_the_empty_trailing_round(renderer, gv, config1):
     finally:
         renderer.set_stats(False)
     assert sf["rounds"] < sl["rounds"], (sf["rounds"], sl["rounds"])
-    fa, fb = fast["rgba32f"].reshape(-1, 4), lit["rgba32f"].reshape(-1, 4)
-    d = np.abs(fa[:, :3] - fb[:, :3]).max(axis=1)
-    assert (d > 1e-4).mean() <= 2e-4 and d.max() <= 0.05
+    _fast_vs_literal(O, config1_enc, fast["rgba32f"], lit["rgba32f"], vi, pi, W, H)
 
 
 def test_literal_stats_match_oracle(renderer, gv, O, config1, config1_enc):
@@ -145,7 +172,7 @@ def test_rt_variant_and_odd_sizes(renderer, gv, O, config1, config1_enc):
         vi, pi = gv.scene.config1_camera(W, H)
         out = renderer.render(vi, pi, W, H, pixel_offset=0.5, alpha_init=1.0)
         ref = O.render(config1_enc, vi, pi, W, H, proxy_mode=1, pixel_offset=0.5, alpha_init=1.0)
-        _cmp_images(out["rgba32f"], ref["rgba32f"], frac_tol=0.02)
+        _cmp_images(out["rgba32f"], ref)
         assert (out["rgba8"][..., 3] == 255).all()  # RT pipeline: alpha starts at 1
 
 
@@ -157,7 +184,7 @@ def test_light_field_ring(renderer, gv, O, config1, config1_enc):
     out = renderer.render(vi, pi, W, H, ncams=4, pixel_offset=0.5, alpha_init=1.0, ray_dirs=True, ray_dirs_layout=1)
     ref = O.render(config1_enc, vi, pi, W, H, ncams=4, proxy_mode=1, pixel_offset=0.5, alpha_init=1.0, ray_dirs=True,
                    ray_dirs_layout=1)
-    _cmp_images(out["rgba32f"], ref["rgba32f"])
+    _cmp_images(out["rgba32f"], ref)
     np.testing.assert_allclose(out["ray_dirs"], ref["ray_dirs"], rtol=0, atol=2e-6)
 
 
@@ -214,7 +241,7 @@ def test_camera_inside_gaussian(gv, O):
         vi, pi = gv.camera.pinhole((0.0, 0.0, 0.5), (0.0, 0.0, -1.0), (0.0, 1.0, 0.0), 60.0, 1.0)
         out = r.render(vi, pi, 8, 8)
     ref = O.render(e, vi, pi, 8, 8, proxy_mode=1)
-    _cmp_images(out["rgba32f"], ref["rgba32f"], frac_tol=0.0)
+    assert _cmp_images(out["rgba32f"], ref, frac_tol=0.0) == 0
     assert (out["rgba32f"][..., 3] == 1.0).all()
 
 
@@ -251,7 +278,7 @@ def test_render_params_vs_oracle(renderer, gv, O, config1, config1_enc, mode, kw
     okw = {k: v for k, v in kw.items() if k != "kbuffer_depth"}
     out = renderer.render(vi, pi, W, H, mode=mode, **kw)
     ref = O.render(config1_enc, vi, pi, W, H, proxy_mode=1, **okw)
-    _cmp_images(out["rgba32f"], ref["rgba32f"])
+    _cmp_images(out["rgba32f"], ref)
 
 
 @pytest.mark.parametrize("kmin", [0.0113, 0.05])
@@ -268,7 +295,7 @@ def test_adaptive_kernel_clamping_vs_oracle(renderer, gv, O, config1, kmin):
     for mode in (0, 1):
         out = renderer.render(vi, pi, W, H, mode=mode)
         ref = O.render(e, vi, pi, W, H, proxy_mode=1, kernel_min_response=kmin, kernel_opts=1)
-        _cmp_images(out["rgba32f"], ref["rgba32f"])
+        _cmp_images(out["rgba32f"], ref)
 
 
 @pytest.mark.parametrize("seed", [11, 12, 13, 14, 15, 16])
@@ -289,7 +316,7 @@ def test_random_scenes_and_cameras_vs_oracle(gv, O, seed):
         assert r.prepare(s) == e["m"]
         for mode in (gv.MODE_FAST, gv.MODE_LITERAL):
             out = r.render(vi, pi, W, H, mode=mode, **kw)
-            _cmp_images(out["rgba32f"], ref["rgba32f"], frac_tol=2e-3)
+            _cmp_images(out["rgba32f"], ref)
         r.set_stats(True)
         r.render(vi, pi, W, H, mode=gv.MODE_LITERAL, **kw)
         st = r.stats()
@@ -311,7 +338,8 @@ def test_hip_reproduces_golden_config1(renderer, gv, config1):
     np.testing.assert_array_equal(g["sh"][: z["sh_head"].size], z["sh_head"].reshape(-1))
     vi, pi = z["view_inv"], z["proj_inv"]
     for mode in (gv.MODE_FAST, gv.MODE_LITERAL):
-        _cmp_images(renderer.render(vi, pi, 64, 64, mode=mode)["rgba32f"], z["rgba_analytic"])
+        _cmp_images(renderer.render(vi, pi, 64, 64, mode=mode)["rgba32f"], z["rgba_analytic"],
+                    margin=z["margin_analytic"])
     renderer.set_stats(True)
     try:
         renderer.render(vi, pi, 64, 64, mode=gv.MODE_LITERAL)
@@ -422,17 +450,16 @@ def test_bicycle_subset_vs_oracle_and_fast_literal(gv, O, bicycle):
         lit = r.render(vi, pi, W, H, mode=gv.MODE_LITERAL)
         again = r.render(vi, pi, W, H)
     assert m > 900_000
-    # FAST == LITERAL except where two crossings have bitwise-equal t across a 16-hit round boundary:
-    # the reference (exclusive tmin) then skips the tied crossing, and FAST's rounds fall elsewhere.
-    diff = np.abs(fast["rgba8"].astype(np.int32) - lit["rgba8"].astype(np.int32))
-    assert (diff.max(axis=-1) > 0).mean() <= 1e-5 and diff.max() <= 8, ((diff > 0).sum(), diff.max())
     np.testing.assert_array_equal(fast["rgba32f"], again["rgba32f"])
     e = O.enclose(bicycle)
     assert e["m"] == m
+    # FAST == LITERAL on every ray but flagged ties / threshold rays (each differing ray re-marched)
+    n = _fast_vs_literal(O, e, fast["rgba32f"], lit["rgba32f"], vi, pi, W, H)
+    assert n <= 1e-4 * W * H, n
     sub = np.arange(0, W * H, 997, dtype=np.uint64)  # ~2 k rays spread over the frame
     ref = O.render(e, vi, pi, W, H, proxy_mode=1, subset=sub)
     got = fast["rgba32f"].reshape(-1, 4)[sub.astype(np.int64)]
-    _cmp_images(got, ref["rgba32f"], frac_tol=5e-3)
+    _cmp_images(got, ref)
     assert gv.psnr_rgb(gv.quantize_rgba8(got), gv.quantize_rgba8(ref["rgba32f"])) >= 50.0
 
 

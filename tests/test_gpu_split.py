@@ -47,7 +47,7 @@ def test_split_config1_equals_unsplit(gv, O, config1, config1_enc, cells):
     for k in ("crossings", "accepted"):
         assert abs(int(st1[k]) - int(st0[k])) <= 1e-4 * st0[k] + 2, (k, st1[k], st0[k])
     ref = O.render(config1_enc, vi, pi, W, H, proxy_mode=1)
-    _cmp_images(out["rgba32f"], ref["rgba32f"])
+    _cmp_images(out["rgba32f"], ref)
 
 
 def test_split_bicycle_vs_oracle(gv, O):
@@ -68,7 +68,7 @@ def test_split_bicycle_vs_oracle(gv, O):
     e = O.enclose(splats)
     sub = np.arange(0, W * H, 997, dtype=np.uint64)
     ref = O.render(e, vi, pi, W, H, proxy_mode=1, subset=sub)
-    _cmp_images(out["rgba32f"].reshape(-1, 4)[sub.astype(np.int64)], ref["rgba32f"], frac_tol=5e-3)
+    _cmp_images(out["rgba32f"].reshape(-1, 4)[sub.astype(np.int64)], ref)
 
 
 def test_split_tiny_scenes_and_limits(gv, O):

@@ -22,11 +22,16 @@ def run(*args):
 
 
 def mats(out):
+    """name -> 16 uint32 bit patterns (glm memory order) as gvrt_app cameras prints them."""
     d = {}
     for line in out.splitlines():
         k, *v = line.split()
-        d[k] = np.array([float(x) for x in v], np.float32)
+        d[k] = np.array([int(x, 16) for x in v], np.uint32)
     return d
+
+
+def bits(m):
+    return np.asarray(m, np.float32).reshape(16).view(np.uint32)
 
 
 def test_usage_and_png_roundtrip(tmp_path):
@@ -44,21 +49,24 @@ def test_usage_and_png_roundtrip(tmp_path):
 
 
 def test_camera_presets_match_python(gv):
-    W, H = 64, 48
-    m = mats(run("cameras", "--width", str(W), "--height", str(H)))
-    vi, pi = gv.scene.config1_camera(W, H)
-    np.testing.assert_allclose(m["config1_view_inv"], vi, rtol=1e-6, atol=1e-6)
-    np.testing.assert_allclose(m["config1_proj_inv"], pi, rtol=1e-6, atol=1e-6)
-    vi, pi = gv.scene.mipnerf_camera(W, H)
-    np.testing.assert_allclose(m["orbit_view_inv"], vi, rtol=1e-6, atol=1e-6)
-    np.testing.assert_allclose(m["orbit_proj_inv"], pi, rtol=1e-6, atol=1e-6)
-    c = gv.camera.Camera()
-    c.set_position((0.5, -1.0, 2.0))
-    c.set_rotation((10.0, 20.0, 30.0))
-    np.testing.assert_allclose(m["euler_view"], gv.camera.colmajor(c.view), rtol=1e-6, atol=1e-6)
+    """C++ (gvrt_math.h, float32 glm order) == Python (camera.py), bit for bit."""
+    cam = gv.camera
+    for W, H in ((64, 48), (1920, 1080)):
+        m = mats(run("cameras", "--width", str(W), "--height", str(H), "--position", "0.5,-1,2", "--rotation", "10,20,30"))
+        vi, pi = gv.scene.config1_camera(W, H)
+        assert np.array_equal(m["config1_view_inv"], bits(vi)) and np.array_equal(m["config1_proj_inv"], bits(pi))
+        vi, pi = gv.scene.mipnerf_camera(W, H)
+        assert np.array_equal(m["orbit_view_inv"], bits(vi)) and np.array_equal(m["orbit_proj_inv"], bits(pi))
+        c = cam.Camera()
+        c.setPerspective(cam.FOV_Y, cam.aspect_ratio(W, H), cam.NEAR_PLANE, cam.FAR_PLANE)
+        c.setPosition((0.5, -1.0, 2.0))
+        c.setRotation((10.0, 20.0, 30.0))
+        vi, pi = c.matrices_inverse()
+        assert np.array_equal(m["euler_view"], bits(c.matrices.view))
+        assert np.array_equal(m["euler_view_inv"], bits(vi)) and np.array_equal(m["euler_proj_inv"], bits(pi))
 
 
-def test_nerf_transforms_loader_matches_python(gv, tmp_path):
+def test_nerf_transforms_and_ring_rig_match_python(gv, tmp_path):
     frames = []
     rng = np.random.default_rng(5)
     for k in range(3):
@@ -68,8 +76,82 @@ def test_nerf_transforms_loader_matches_python(gv, tmp_path):
         frames.append({"file_path": f"./val/r_{k}", "rotation": 0.01, "transform_matrix": c2w.tolist()})
     tj = tmp_path / "transforms_val.json"
     tj.write_text(json.dumps({"camera_angle_x": 0.6911112070083618, "frames": frames}, indent=4))
-    m = mats(run("cameras", "--transforms", str(tj)))
-    angle, views = gv.camera.load_nerf_cameras(str(tj))
-    assert math.isclose(angle, 0.6911112070083618)
-    for k, w2c in enumerate(views):
-        np.testing.assert_allclose(m[f"nerf_w2c_{k}"], gv.camera.colmajor(w2c), rtol=1e-6, atol=1e-6)
+    splats = gv.scene.config1(n=500)
+    ply = str(tmp_path / "s.ply")
+    gv.save_ply(ply, splats)
+    W, H = 800, 600
+    m = mats(run("cameras", "--width", str(W), "--height", str(H), "--transforms", str(tj), "--ply", ply))
+    vis, pi = gv.camera.nerf_eval_matrices(str(tj), W, H)
+    _, w2cs = gv.camera.load_nerf_cameras(str(tj), W, H)
+    for k in range(3):
+        assert np.array_equal(m[f"nerf_w2c_{k}"], bits(w2cs[k]))
+        assert np.array_equal(m[f"nerf_view_inv_{k}"], bits(vis[k]))
+        assert np.array_equal(m[f"nerf_proj_inv_{k}"], bits(pi))
+    vi, pi = gv.camera.lightfield_ring_rig(splats["positions"], 4, W, H)
+    for c in range(4):
+        assert np.array_equal(m[f"ring_view_inv_{c}"], bits(vi[16 * c:16 * c + 16]))
+    assert np.array_equal(m["ring_proj_inv"], bits(pi))
+
+
+REF_CAM = os.path.join(ROOT, "oracle", "_ref", "ref_camera_dump")
+
+
+@pytest.mark.skipif(not os.path.exists(REF_CAM), reason="oracle/_ref not built (needs /root/reference)")
+def test_cpp_cameras_bit_identical_to_reference(gv, tmp_path):
+    """gvrt_app's Camera / CameraLoader / light-field rig against the reference's own camera.hpp /
+    LoadCamera.hpp / glm built from its sources (oracle/_ref/ref_camera_dump)."""
+    def hx(*v):
+        return " ".join(float(np.float32(x)).hex() for x in v)
+
+    tj = tmp_path / "transforms_val.json"
+    tj.write_text(json.dumps({"camera_angle_x": 0.5, "frames": [
+        {"file_path": "a", "transform_matrix": [[0.6, -0.8, 0.0, 1.5], [0.8, 0.6, 0.0, -2.25], [0.0, 0.0, 1.0, 3.0],
+                                                [0.0, 0.0, 0.0, 1.0]]}]}))
+    splats = gv.scene.config1(n=400)
+    ply = str(tmp_path / "s.ply")
+    gv.save_ply(ply, splats)
+    pf = tmp_path / "pos.f32"
+    pf.write_bytes(np.ascontiguousarray(splats["positions"], np.float32).tobytes())
+    W, H = 640, 360
+    m = mats(run("cameras", "--width", str(W), "--height", str(H), "--transforms", str(tj), "--ply", ply,
+                 "--position", "1.25,-0.5,3", "--rotation", "-20,35,10"))
+    cam = gv.camera
+    asp = cam.aspect_ratio(W, H)
+    lines = [f"euler {hx(1.25, -0.5, 3, -20, 35, 10, cam.FOV_Y, asp, cam.NEAR_PLANE, cam.FAR_PLANE)}",
+             f"nerf {tj} {W} {H} {hx(cam.NEAR_PLANE)} {hx(cam.FAR_PLANE)}",
+             f"lfring {pf} 400 {W} {H} 4",
+             f"lookat {hx(0, 0, 3, 0, 0, 0, 0, 1, 0)}", f"persp {hx(cam.FOV_Y, asp, cam.NEAR_PLANE, cam.FAR_PLANE)}"]
+    r = subprocess.run([REF_CAM], input="\n".join(lines) + "\n", capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    ref = [np.array([int(x, 16) for x in ln.split()], np.uint32) for ln in r.stdout.splitlines() if len(ln.split()) == 16]
+    assert np.array_equal(m["euler_view"], ref[0]) and np.array_equal(m["euler_view_inv"], ref[1])
+    assert np.array_equal(m["euler_proj_inv"], ref[3])
+    assert np.array_equal(m["nerf_w2c_0"], ref[4]) and np.array_equal(m["nerf_view_inv_0"], ref[5])
+    assert np.array_equal(m["nerf_proj_inv_0"], ref[7])
+    for c in range(4):
+        assert np.array_equal(m[f"ring_view_inv_{c}"], ref[8 + c])
+    assert np.array_equal(m["ring_proj_inv"], ref[12])
+    assert np.array_equal(m["config1_view_inv"], ref[14]) and np.array_equal(m["config1_proj_inv"], ref[16])
+
+
+def test_reference_host_interfaces_compile_and_run(gv, tmp_path):
+    """The reference's host interfaces kept intact (north_star): tests/cpp/host_interfaces.cpp asserts each
+    member-function type and calls it with the reference's argument types; it links libgvrt.so and runs the
+    host-side parts (PLY loader, NeRF camera loader, Camera, vks::Benchmark) without a GPU."""
+    pkg = os.path.join(ROOT, "3dgvrt_lightfield_amd")
+    exe = str(tmp_path / "host_interfaces")
+    r = subprocess.run(["g++", "-O1", "-std=c++17", "-ffp-contract=off", "-Wall", "-Werror", "-I", os.path.join(pkg, "host"),
+                        os.path.join(ROOT, "tests", "cpp", "host_interfaces.cpp"), os.path.join(pkg, "host", "gvrt_host.cpp"),
+                        "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-L", pkg, "-lgvrt", "-L/opt/rocm/lib",
+                        "-lamdhip64", f"-Wl,-rpath,{pkg}", "-Wl,-rpath,/opt/rocm/lib", "-o", exe],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    ply = str(tmp_path / "s.ply")
+    gv.save_ply(ply, gv.scene.config1(n=300))
+    tj = tmp_path / "transforms_val.json"
+    tj.write_text(json.dumps({"camera_angle_x": 0.69, "frames": [
+        {"file_path": "a", "transform_matrix": [[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 1, 4], [0, 0, 0, 1]]}]}))
+    r = subprocess.run([exe, ply, str(tj)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "splats 300 frames 1 cams 1" in r.stdout and "bench 5 5" in r.stdout
+    assert "Benchmark finished" in r.stdout and "device : host-check" in r.stdout

@@ -221,7 +221,7 @@ def test_inclusive_tmin_needs_a_round_cap(gv, O):
 
 def test_camera_math(gv):
     cam = gv.camera
-    P = cam.perspective_vulkan_no_depth_reverse(math.radians(60), 2.0, 0.1, 10.0)
+    P = cam.rowcol(cam.perspective_vulkan_no_depth_reverse(cam.radians(60), 2.0, 0.1, 10.0))
     t = math.tan(math.radians(30))
     assert P[0, 0] == pytest.approx(1 / (2 * t)) and P[1, 1] == pytest.approx(-1 / t)
     assert P[3, 2] == -1 and P[2, 2] == pytest.approx(-10 / 9.9) and P[2, 3] == pytest.approx(-1 / 9.9)
