@@ -439,11 +439,12 @@ def lightfield_ring_rig(positions, ncams=4, width=180, height=180):
 
 
 def lightfield_grid_rig(eye, target, up=(0.0, 1.0, 0.0), nx=4, ny=4, spacing=0.1, fovy_deg=50.0,
-                        aspect=f32(16) / f32(9)):
+                        aspect=f32(16) / f32(9), centred=True):
     """Config 5 camera array: nx*ny pinholes on a plane, parallel look direction, float32:
     f = normalize(target - eye), s = normalize(cross(f, up)), u = cross(s, f); camera (i, j) at
-    eye + (ox * s + oy * u) with ox = (i - (nx-1)/2) * spacing, oy = (j - (ny-1)/2) * spacing, looking at
-    its position + f."""
+    eye + (ox * s + oy * u) with ox = (i - (nx-1)/2) * spacing, oy = (j - (ny-1)/2) * spacing (centred), or
+    ox = i * spacing, oy = j * spacing (centred=False: camera (0, 0) is `eye` itself), looking at its
+    position + f."""
     eye = vec3(eye)
     up = vec3(up)
     f = normalize(sub(vec3(target), eye))
@@ -454,8 +455,8 @@ def lightfield_grid_rig(eye, target, up=(0.0, 1.0, 0.0), nx=4, ny=4, spacing=0.1
     vis = []
     for j in range(ny):
         for i in range(nx):
-            ox = (f32(i) - f32(nx - 1) / f32(2)) * sp
-            oy = (f32(j) - f32(ny - 1) / f32(2)) * sp
+            ox = ((f32(i) - f32(nx - 1) / f32(2)) if centred else f32(i)) * sp
+            oy = ((f32(j) - f32(ny - 1) / f32(2)) if centred else f32(j)) * sp
             pos = add(eye, add(scale(s, ox), scale(u, oy)))
             vis.append(colmajor(inverse(look_at(pos, add(pos, f), up))))
     return np.concatenate(vis), colmajor(inverse(proj))

@@ -1,15 +1,22 @@
-"""Multi-GPU frame split + gather: one process per GPU, scene and LBVH replicated per
+"""Multi-GPU frame split + exchange: one process per GPU, scene and BVH replicated per
 rank, one exchange per frame.
 
-  * tile split  (strong scaling): 64x64-pixel blocks (8x8 of the kernel's 8x8 tiles) round-robin
-    over ranks; each rank renders its tiles tile-packed, the parts are gathered to rank 0 with
-    torch.distributed (backend 'nccl' = RCCL over xGMI on MI355X, 'gloo' on CPU for tests) and
+  * tile split  (strong scaling, config 4): 64x64-pixel blocks (8x8 of the kernel's 8x8 tiles)
+    round-robin over ranks; each rank renders its tiles tile-packed, the parts are gathered to rank 0
+    with torch.distributed (backend 'nccl' = RCCL over xGMI on MI355X, 'gloo' on CPU for tests) and
     scattered into the frame (gvrt_unpack_tiles_rgba8 on the GPU, unpack_tiles_host on the CPU).
   * view split  (weak scaling, light-field config 5): whole views round-robin over ranks.
 
-The renderer is injected (`render_fn`) so the collective plumbing is testable without a GPU.
+`FrameExchange` is the double-buffered exchange bench.py runs; the renderer and the rank-0 assembly are
+injected, so the same object is driven by the gloo tests on CPU (tests/test_dist.py).  `launch_ranks`
+turns `bench.py --gpus N` started as one plain process into N ranks.
 """
 from __future__ import annotations
+
+import os
+import socket
+import subprocess
+import sys
 
 import numpy as np
 
@@ -19,6 +26,11 @@ from .renderer import tiles_for_rank
 def rank_tiles(width, height, ncams, world, block=8):
     """Tile lists of every rank (uint16 [n, 4] rows of (tx, ty, cam, 0))."""
     return [tiles_for_rank(width, height, ncams, r, world, block) for r in range(world)]
+
+
+def rank_views(views, world):
+    """Views of every rank, round-robin (config 5 shards whole views over GPUs)."""
+    return [list(range(r, views, world)) for r in range(world)]
 
 
 def unpack_tiles_host(packed, tiles, width, height, ncams=1, frame=None):
@@ -35,19 +47,73 @@ def unpack_tiles_host(packed, tiles, width, height, ncams=1, frame=None):
     return frame
 
 
-def gather_tiles(dist, part, rank, world, sizes, device=None):
-    """Gather tile-packed parts (uint8 [n_r*64, 4] tensors) to rank 0.  NCCL/gloo gather needs equal
-    shapes, so every part is padded to the largest; rank 0 gets the unpadded list."""
-    import torch
+class FrameExchange:
+    """Double-buffered frame exchange, the one exchange step per frame of SURVEY §8e.
 
-    maxn = max(sizes)
-    send = torch.zeros((maxn, part.shape[1]), dtype=part.dtype, device=part.device)
-    send[: part.shape[0]].copy_(part)
-    bufs = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
-    dist.gather(send, bufs, dst=0)
-    if rank != 0:
-        return None
-    return [b[:s] for b, s in zip(bufs, sizes)]
+    Every rank owns `nbuf` send buffers of one padded part shape (collective gathers need equal shapes:
+    the largest rank's part).  step(render) waits until the gather that last used buffer b has completed
+    (and lets rank 0 assemble that frame), renders the next frame into buffer b, and posts its gather to
+    rank 0 asynchronously, so the gather of frame i (RCCL on torch's stream) overlaps the render of frame
+    i + 1 (the library's HIP stream).  drain() completes every outstanding frame.
+
+      render(buf)             writes this rank's part of the next frame into `buf` (a view of the send
+                              buffer of this rank's own part size)
+      assemble(parts, frame)  rank 0 only: builds the frame from the gathered parts (list of world tensors,
+                              each cut to its rank's part size); frame counts from 0
+      sync()                  called after a gather completed and before its buffers are reused or read
+                              by another stream (torch.cuda.current_stream().synchronize on the GPU)
+    """
+
+    def __init__(self, dist, rank, world, part_sizes, item_shape, dtype, device="cpu", nbuf=2, assemble=None,
+                 sync=None):
+        import torch
+
+        self.dist, self.rank, self.world = dist, rank, world
+        self.part_sizes = [int(s) for s in part_sizes]
+        maxn = max(self.part_sizes)
+        shape = (maxn,) + tuple(item_shape)
+        self.send = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(nbuf)]
+        self.recv = [[torch.empty(shape, dtype=dtype, device=device) for _ in range(world)] if rank == 0 else None
+                     for _ in range(nbuf)]
+        self.pending = [None] * nbuf
+        self.frame_of = [None] * nbuf
+        self.nbuf = nbuf
+        self.assemble = assemble
+        self.sync = sync
+        self.frames = 0
+
+    def _finish(self, b):
+        if self.pending[b] is None:
+            return
+        self.pending[b].wait()
+        if self.sync:
+            self.sync()
+        if self.rank == 0 and self.assemble:
+            self.assemble([p[:n] for p, n in zip(self.recv[b], self.part_sizes)], self.frame_of[b])
+        self.pending[b] = None
+
+    def step(self, render):
+        b = self.frames % self.nbuf
+        self._finish(b)
+        render(self.send[b][: self.part_sizes[self.rank]])
+        self.pending[b] = self.dist.gather(self.send[b], self.recv[b] if self.rank == 0 else None, dst=0,
+                                           async_op=True)
+        self.frame_of[b] = self.frames
+        self.frames += 1
+
+    def drain(self):
+        for k in range(self.nbuf):
+            self._finish((self.frames + k) % self.nbuf)
+
+
+def gather_tiles(dist, part, rank, world, sizes, device=None):
+    """Gather tile-packed parts (uint8 [n_r*64, 4] tensors) to rank 0 (one synchronous exchange)."""
+    ex = FrameExchange(dist, rank, world, sizes, part.shape[1:], part.dtype, part.device, nbuf=1)
+    out = []
+    ex.assemble = lambda parts, _f: out.extend(parts)
+    ex.step(lambda buf: buf.copy_(part))
+    ex.drain()
+    return out if rank == 0 else None
 
 
 def render_split_frame(dist, render_fn, width, height, rank, world, block=8, device="cpu", unpack_fn=None):
@@ -73,3 +139,33 @@ def render_split_frame(dist, render_fn, width, height, rank, world, block=8, dev
     for p, t in zip(parts, all_tiles):
         unpack_fn(p, t, frame)
     return frame
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(nproc, script, argv, env=None):
+    """One process per GPU: when `script --gpus N` runs as a plain process (no WORLD_SIZE, or WORLD_SIZE 1)
+    with N > 1, start its N ranks as children (`torch.distributed.run`, one node, rendezvous on 127.0.0.1)
+    and return their exit code.  Returns None when this process already is one rank of an N-rank job (or
+    N == 1): the caller then goes on as that rank.  A job whose WORLD_SIZE is neither 1 nor N is refused.
+    Call before anything touches the GPU (the children do the GPU work; nothing here is exec'd)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == nproc:
+        return None
+    if world > 1:
+        raise SystemExit(f"launched with WORLD_SIZE={world} but --gpus {nproc}")
+    if nproc <= 1:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", script, *argv]
+    e = dict(os.environ if env is None else env)
+    e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only (RCCL / tensor sharing across ranks)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    return subprocess.run(cmd, env=e).returncode

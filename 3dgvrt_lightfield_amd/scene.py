@@ -62,7 +62,7 @@ def config1_camera(width=256, height=256):
     return cam.pinhole((0.0, 0.0, 3.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), cam.FOV_Y, cam.aspect_ratio(width, height))
 
 
-def mipnerf_standin(n=1_000_000, seed=1):
+def mipnerf_standin(n=1_000_000, seed=1, scale_mult=1.0, opacity_mean=1.0, opacity_std=2.0):
     """Configs 2-5 stand-in: 60% in an object ball (radius 1.5), 40% in a background
     shell r in [3, 15] with scale proportional to r; log-scale N(ln(0.008 * r_rel), 0.5) with
     r_rel = 1 in the object and r/1.5 in the shell; opacity logit N(1, 2); SH degree 3 as config 1;
@@ -80,11 +80,18 @@ def mipnerf_standin(n=1_000_000, seed=1):
     pos_b = d * rb[:, None]
     pos = np.concatenate([pos_o, pos_b])
     r_rel = np.concatenate([np.ones(n_obj), rb / 1.5])
-    log_scale = rng.normal(np.log(0.008 * r_rel)[:, None], 0.5, (n, 3))
-    opacity = rng.normal(1.0, 2.0, n)
+    log_scale = rng.normal(np.log(0.008 * scale_mult * r_rel)[:, None], 0.5, (n, 3))
+    opacity = rng.normal(opacity_mean, opacity_std, n)
     f_dc = 0.8 * np.sin(2.0 * pos) + rng.normal(0.0, 0.3, (n, 3))
     perm = rng.permutation(n)  # PLY order is not spatially sorted
     return _finish(rng, n, pos[perm], log_scale[perm], opacity[perm], f_dc[perm], frac_filter=0.01)
+
+
+def dense_standin(n=1_000_000, seed=4, scale_mult=3.5, opacity_mean=-3.0):
+    """Dense stand-in ("hundreds of crossings per ray"): the config-2 generator with
+    scales x3.5 and opacity logit N(-3, 2), seed 4.  Oracle counters at 1920x1080 (every 2003rd ray):
+    151.7 crossings, 78.7 accepted and 9.95 LITERAL rounds per ray (vs 22.1 / 17.7 / 1.85 for config 2)."""
+    return mipnerf_standin(n, seed, scale_mult=scale_mult, opacity_mean=opacity_mean)
 
 
 def mipnerf_camera(width=1920, height=1080, azimuth_deg=30.0):
@@ -99,6 +106,7 @@ CONFIGS = {
     "garden": (dict(kind="mipnerf", n=3_000_000, seed=2), 1920, 1080, 1),
     "truck": (dict(kind="mipnerf", n=2_000_000, seed=3), 3840, 2160, 1),
     "lightfield": (dict(kind="mipnerf", n=1_000_000, seed=1), 1920, 1080, 16),
+    "dense": (dict(kind="dense", n=1_000_000, seed=4), 1920, 1080, 1),
 }
 
 
@@ -107,6 +115,8 @@ def make(kind="config1", n=10_000, seed=CONFIG1_SEED):
         return config1(n, seed)
     if kind == "mipnerf":
         return mipnerf_standin(n, seed)
+    if kind == "dense":
+        return dense_standin(n, seed)
     raise ValueError(kind)
 
 

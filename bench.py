@@ -6,20 +6,34 @@ Workload at N=1: config 2 ("bicycle" stand-in, 1M synthetic Gaussians, seed 1, 1
 camera r=4 / elev 20 / fovy 50, ray-query variant).  A step = one Particle Rendering pass over one
 1920x1080 view with the scene, proxies and BVH resident in HBM (enclosing + BVH build are
 one-shot and reported separately; by default the static-scene quality build, `--build fast` for the
-1.4 ms device LBVH).  With --gpus N each rank renders its own view of an N-camera
-light-field rig (config 5 shards views over GPUs) and the frames are gathered to rank 0 with RCCL
-(torch.distributed 'nccl'): per-GPU work is fixed, so scaling is weak.  `--split tiles` instead
-splits ONE frame into 64x64 blocks round-robin over ranks (strong scaling) and gathers the
-tile-packed parts.
+millisecond device LBVH).
+
+Several GPUs: `python bench.py --gpus N` started as one process launches its N ranks
+itself (torch.distributed.run, one process per GPU; dist.launch_ranks); launched by torch.distributed.run
+with WORLD_SIZE = N it is one of them.  `--split views` (default; config 5) gives each rank its own
+view(s) of a light-field camera rig: weak scaling.  `--split tiles` (default for `--config truck`,
+config 4) splits ONE frame into 64x64 blocks round-robin over ranks: strong scaling.  Either way the
+ranks' parts go to rank 0 through dist.FrameExchange (double-buffered RCCL gather, tile parts scattered
+into the frame by gvrt_unpack_tiles_rgba8).
+
+At N=1 the line also carries the HBM traffic of the render kernel measured by rocprofv3 PMC passes of
+this same command (FETCH_SIZE, WRITE_SIZE, VALU issue; child processes started before this process
+touches the GPU), and the CPU baseline (the oracle restatement on the host's CPU share).
 
     python bench.py --gpus 1 --steps 20 --warmup 3
 """
 import argparse
+import csv
+import glob
+import hashlib
 import importlib
 import json
 import math
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -28,6 +42,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table
+# VALU issue: 256 CUs x 4 SIMDs x 2.4 GHz, one wave64 VALU instruction per 2 cycles per SIMD (MI355X_MICROARCH.md)
+VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2
 
 
 def parse():
@@ -35,35 +51,126 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="bicycle", choices=["bicycle", "garden", "truck", "lightfield", "config1"])
-    ap.add_argument("--split", default="views", choices=["views", "tiles"])
+    ap.add_argument("--config", default="bicycle",
+                    choices=["bicycle", "garden", "truck", "lightfield", "config1", "dense"])
+    ap.add_argument("--split", default="auto", choices=["auto", "views", "tiles"],
+                    help="auto: tiles for --config truck (config 4, strong scaling), else views")
     ap.add_argument("--mode", default="fast", choices=["fast", "literal"])
     ap.add_argument("--ply", default=None, help="render this 3DGS .ply (e.g. Mip-NeRF360 bicycle) instead of the "
                                                   "synthetic stand-in of --config (same camera and resolution)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true", help="skip the LITERAL stats pass (roofline bytes)")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes (roofline.traffic, VALU)")
     ap.add_argument("--build", default="quality", choices=["quality", "fast"],
-                    help="quality: host binned-SAH tree + SAH-optimal 4-wide collapse (the static-scene build, as "
-                         "the reference's PREFER_FAST_TRACE BLAS); fast: device LBVH + greedy collapse (~1.4 ms)")
-    return ap.parse_args()
+                    help="quality: binned-SAH tree + SAH-optimal 4-wide collapse (the static-scene build, as "
+                         "the reference's PREFER_FAST_TRACE BLAS); fast: device LBVH + greedy collapse")
+    args = ap.parse_args()
+    if args.split == "auto":
+        args.split = "tiles" if args.config == "truck" else "views"
+    return args
+
+
+# ------------------------------------------------------------------------------------------------ host
+def cpu_share():
+    """CPUs this job may use on the host (affinity, cgroup quota, OMP_NUM_THREADS) and the node's CPU model."""
+    n_aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = n_aff
+    if quota:
+        threads = min(threads, max(1, int(math.floor(quota))))
+    if omp and omp.isdigit():
+        threads = min(threads, int(omp))
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"threads": max(1, threads), "nproc": os.cpu_count(), "affinity": n_aff, "cgroup_quota_cpus": quota,
+            "omp_num_threads": omp, "model": model}
+
+
+# ------------------------------------------------------------------------------------------------ PMC
+def pmc_passes(args):
+    """roofline.traffic and the VALU-issue roofline from rocprofv3 PMC passes of THIS command (a short run:
+    5 timed + 1 warmup FAST launches, no CPU baseline / stats), one counter set per pass as MI355X_MICROARCH.md
+    prescribes (FETCH_SIZE and WRITE_SIZE cannot share a pass).  Runs as child processes before this process
+    touches the GPU.  Returns per-dispatch averages of the k_render kernel, or {"error": ...}."""
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return {"error": "rocprofv3 not found"}
+    child = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", "5", "--warmup", "1",
+             "--config", args.config, "--split", args.split, "--mode", args.mode, "--build", args.build,
+             "--no-cpu-baseline", "--no-stats", "--no-pmc"]
+    if args.ply:
+        child += ["--ply", args.ply]
+    out = {}
+    passes = [["FETCH_SIZE"], ["WRITE_SIZE"], ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM"]]
+    tmp = tempfile.mkdtemp(prefix="gvrt_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        for i, counters in enumerate(passes):
+            d = os.path.join(tmp, f"p{i}")
+            cmd = ["timeout", "-s", "KILL", "150", exe, "--pmc", *counters, "--kernel-include-regex", "k_render",
+                   "-d", d, "-o", "run", "--output-format", "csv", "--", *child]
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True, timeout=200,
+                               env=dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp")))
+            files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            if r.returncode != 0 or not files:
+                out.setdefault("error", f"pass {counters}: rc {r.returncode} {r.stderr[-300:]}")
+                break
+            agg, cnt = {}, {}
+            for f in files:
+                for row in csv.DictReader(open(f)):
+                    if "k_render" not in row.get("Kernel_Name", ""):
+                        continue
+                    k = row["Counter_Name"]
+                    agg[k] = agg.get(k, 0.0) + float(row["Counter_Value"])
+                    cnt[k] = cnt.get(k, 0) + 1
+            out.update({k: agg[k] / cnt[k] for k in agg})
+            out["dispatches"] = max(cnt.values()) if cnt else 0
+    except subprocess.TimeoutExpired:
+        out.setdefault("error", "PMC pass timed out")
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return out
 
 
 def main():
     args = parse()
+    dist_mod = importlib.import_module("3dgvrt_lightfield_amd.dist")  # no GPU work at import
+    rc = dist_mod.launch_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+    if rc is not None:  # this process started the N ranks; rank 0 printed the line
+        sys.exit(rc)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        world = max(world, 1)
+    distributed = world > 1
+    pmc = None
+    if not distributed and not args.no_pmc:
+        pmc = pmc_passes(args)  # before this process touches the GPU
+
     import torch
     import torch.distributed as dist
 
     gv = importlib.import_module("3dgvrt_lightfield_amd")
-    distributed = world > 1
     if distributed:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        world = dist.get_world_size()
+        rank = dist.get_rank()
+    if world != args.gpus:
+        print(f"bench: {world} ranks but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     dev = torch.device("cuda", local_rank)
 
     gen, W, H, ncams_cfg = gv.scene.CONFIGS[args.config]
@@ -82,94 +189,77 @@ def main():
     m = r.prepare(splats, **bkw)    # steady-state scene build (what a scene change costs)
     st0 = r.stats()
 
-    # cameras: an N-view planar rig around the config-2 orbit camera (view 0 = the config camera)
+    # cameras: an N-view planar rig starting at the config camera (view 0 = the config camera for any N);
+    # config 5 (lightfield) is its centred 16-view array
     if args.config == "config1":
         eye, fovy = (0.0, 0.0, 3.0), gv.camera.FOV_Y
     else:
         eye, fovy = gv.camera.orbit_eye(4.0, 20.0, 30.0), 50.0  # = scene.mipnerf_camera (view 0)
-    target = (0.0, 0.0, 0.0)
     views = world if args.split == "views" else 1
     views = max(views, ncams_cfg if args.config == "lightfield" else 1)
-    vis, pi = gv.camera.lightfield_grid_rig(eye, target, (0.0, 1.0, 0.0), nx=views, ny=1, spacing=0.1,
-                                            fovy_deg=fovy, aspect=gv.camera.aspect_ratio(W, H))
+    vis, pi = gv.camera.lightfield_grid_rig(eye, (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), nx=views, ny=1, spacing=0.1,
+                                            fovy_deg=fovy, aspect=gv.camera.aspect_ratio(W, H),
+                                            centred=args.config == "lightfield")
     vis = vis.reshape(views, 16)
+    mode = gv.MODE_FAST if args.mode == "fast" else gv.MODE_LITERAL
+    params = r.render_params(mode=mode)
     if args.split == "views":
-        my_views = [v for v in range(views) if v % world == rank]
+        all_views = dist_mod.rank_views(views, world)
+        my_views = all_views[rank]
         vi = np.ascontiguousarray(vis[my_views].reshape(-1))
         ncams = len(my_views)
         tiles = None
         rays_per_rank = W * H * ncams
-        frame = torch.zeros((ncams, H, W, 4), dtype=torch.uint8, device=dev)
+        part_sizes, item_shape = [len(v) for v in all_views], (H, W, 4)
     else:
         vi = np.ascontiguousarray(vis[0])
         ncams = 1
-        tiles = gv.tiles_for_rank(W, H, 1, rank, world, block=8)
+        all_tiles = dist_mod.rank_tiles(W, H, 1, world, block=8)
+        tiles = all_tiles[rank]
         rays_per_rank = int(tiles.shape[0]) * 64
-        frame = torch.zeros((tiles.shape[0] * 64, 4), dtype=torch.uint8, device=dev)
-    mode = gv.MODE_FAST if args.mode == "fast" else gv.MODE_LITERAL
-    params = r.render_params(mode=mode)
-
-    # Double-buffered frame exchange: the RCCL gather of frame i (torch's stream, async) runs while
-    # frame i+1 renders on the library's own HIP stream; a buffer is reused only after its gather
-    # completed.  Tile split: rank 0 scatters the gathered parts into the full frame
-    # (gvrt_unpack_tiles_rgba8), as SURVEY §8e's one exchange step per frame.
-    nbuf = 2 if distributed else 1
-    frames = [frame] + [torch.zeros_like(frame) for _ in range(nbuf - 1)]
-    rank_tiles = [gv.tiles_for_rank(W, H, 1, q, world, block=8) for q in range(world)] if args.split == "tiles" else None
-    if distributed and args.split == "tiles":
-        # NCCL gather needs equal sizes: pad every rank's part to the largest
-        maxs = max(t.shape[0] for t in rank_tiles) * 64
-        sendbufs = [torch.zeros((maxs, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
-        gathered = [[torch.empty((maxs, 4), dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
-                    for _ in range(nbuf)]
-        full = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
-    elif distributed:
-        gathered = [[torch.empty_like(frame) for _ in range(world)] if rank == 0 else None for _ in range(nbuf)]
-    pending = [None] * nbuf
-
+        part_sizes, item_shape = [t.shape[0] * 64 for t in all_tiles], (4,)
+    packed = args.split == "tiles"
     kernel_ms = []
+    full = None
 
-    def finish(b):
-        if pending[b] is None:
-            return
-        pending[b].wait()
-        torch.cuda.current_stream().synchronize()  # the library's stream reads / overwrites this buffer next
-        if args.split == "tiles" and rank == 0:
-            for q in range(world):
-                r.unpack_tiles_rgba8(gathered[b][q].data_ptr(), rank_tiles[q], W, H, full.data_ptr())
-        pending[b] = None
+    if distributed:
+        # one exchange step per frame: dist.FrameExchange, double-buffered RCCL gather to rank 0
+        if packed and rank == 0:
+            full = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
 
-    it = [0]
+        def assemble(parts, _frame):  # rank 0: tile parts -> the frame (gvrt_unpack_tiles_rgba8)
+            if packed:
+                for p, t in zip(parts, all_tiles):
+                    r.unpack_tiles_rgba8(p.data_ptr(), t, W, H, full.data_ptr())
 
-    # One GPU: frames are queued back to back (gvrt_render_async; one host round trip per K frames instead of
-    # one per frame); the kernel time is the mean over the queued launches (HIP event pairs), read at sync.
-    # Several ranks: synchronous renders, each frame handed to the RCCL gather as soon as it is done.
-    use_async = not distributed
+        ex = dist_mod.FrameExchange(dist, rank, world, part_sizes, item_shape, torch.uint8, dev, nbuf=2,
+                                    assemble=assemble, sync=lambda: torch.cuda.current_stream().synchronize())
 
-    def step():
-        b = it[0] % nbuf
-        it[0] += 1
-        finish(b)
-        r.render_device(vi, pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=frames[b].data_ptr(),
-                        packed=args.split == "tiles", async_=use_async)
-        if not use_async:
+        def render_into(buf):  # synchronous render on the library's stream, straight into the send buffer
+            r.render_device(vi, pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=buf.data_ptr(), packed=packed)
             kernel_ms.append(r.render_ms())
-        if distributed:
-            if args.split == "views":
-                pending[b] = dist.gather(frames[b], gathered[b] if rank == 0 else None, dst=0, async_op=True)
-            else:
-                sendbufs[b][: frames[b].shape[0]].copy_(frames[b])
-                pending[b] = dist.gather(sendbufs[b], gathered[b] if rank == 0 else None, dst=0, async_op=True)
 
-    def drain():
-        for b in range(nbuf):
-            finish(b)
+        def step():
+            ex.step(render_into)
+
+        def drain():
+            ex.drain()
+    else:
+        # One GPU: frames are queued back to back (gvrt_render_async; one host round trip per K frames instead
+        # of one per frame); the kernel time is the mean over the queued launches (HIP event pairs), at sync.
+        frame = torch.zeros((part_sizes[0],) + item_shape, dtype=torch.uint8, device=dev)
+
+        def step():
+            r.render_device(vi, pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=frame.data_ptr(),
+                            packed=packed, async_=True)
+
+        def drain():
+            r.sync()
+            kernel_ms.append(r.render_ms())  # mean over the queued launches
 
     for _ in range(args.warmup):
         step()
     drain()
-    if use_async:
-        r.sync()
     kernel_ms.clear()
     if distributed:
         dist.barrier()
@@ -177,10 +267,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    drain()  # every frame of the timed steps is rendered and gathered (and scattered) inside the clock
-    if use_async:
-        r.sync()  # every queued frame finished inside the clock
-        kernel_ms.append(r.render_ms())  # mean over the K launches
+    drain()  # every frame of the timed steps is rendered (and gathered and assembled) inside the clock
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
@@ -199,7 +286,21 @@ def main():
     mrays = total_rays_per_step * args.steps / elapsed / 1e6
     kern_avg = float(np.mean(kernel_ms)) if kernel_ms else float("nan")
 
-    result = None
+    # digest of view 0 as rank 0 holds it after the exchange (tile split: the assembled frame, equal for any N)
+    digest = None
+    if rank == 0:
+        if distributed:
+            img = full if packed else ex.recv[(ex.frames - 1) % ex.nbuf][0][0]
+        else:
+            img = frame if not packed else None
+            if packed:  # one rank: unpack the whole frame's tiles
+                img = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
+                r.unpack_tiles_rgba8(frame.data_ptr(), tiles, W, H, img.data_ptr())
+            else:
+                img = frame[0]
+        torch.cuda.synchronize()
+        digest = hashlib.sha1(img.cpu().numpy().tobytes()).hexdigest()
+
     if rank == 0:
         # ---- roofline: algorithmic bytes of the reference algorithm on this input (LITERAL counters)
         roof = None
@@ -214,25 +315,34 @@ def main():
                 rays_per_rank / rays1)
             achieved = bytes_per_launch / (kern_avg * 1e-3) / 1e9
             traffic = None
-            pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
-            if os.path.exists(pmc):
-                try:
-                    traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-                except Exception:
-                    traffic = None
+            if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+                # FETCH_SIZE in KiB, half-counted on gfx950 (x2); WRITE_SIZE in KiB (MI355X_MICROARCH.md, HBM)
+                traffic = pmc["FETCH_SIZE"] * 1024 * 2 + pmc["WRITE_SIZE"] * 1024
             roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                     "algorithmic_bytes_per_launch": bytes_per_launch,
                     "kernel_ms_avg": round(kern_avg, 4), "kernel": "k_render<FAST,K=24,packed>"}
+            if pmc:
+                roof["pmc"] = {k: v for k, v in pmc.items()}
+                if traffic is not None:
+                    roof["traffic_read_bytes"] = pmc["FETCH_SIZE"] * 1024 * 2
+                    roof["traffic_write_bytes"] = pmc["WRITE_SIZE"] * 1024
+                if "SQ_INSTS_VALU" in pmc:
+                    rate = pmc["SQ_INSTS_VALU"] / (kern_avg * 1e-3)
+                    roof["valu_issue"] = {"achieved": rate, "peak": VALU_PEAK_WAVE_INSTR, "unit": "wave-instr/s",
+                                          "frac": round(rate / VALU_PEAK_WAVE_INSTR, 4),
+                                          "valu_per_wave": pmc["SQ_INSTS_VALU"] / max(pmc.get("SQ_WAVES", 1), 1),
+                                          "salu_per_wave": pmc.get("SQ_INSTS_SALU", 0) / max(pmc.get("SQ_WAVES", 1), 1)}
 
-        # ---- CPU baseline (oracle restatement, all host threads we use), PSNR vs oracle on the sample
+        # ---- CPU baseline (oracle restatement on the host's CPU share), PSNR vs oracle on the sample
         cpu = None
         psnr = None
         if not args.no_cpu_baseline and world == 1:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle as O
 
-            threads = min(16, os.cpu_count() or 1)
+            host = cpu_share()
+            threads = host["threads"]
             e = O.enclose(splats)
             sc = O.Scene(e, proxy_mode=1)
             probe = np.arange(0, W * H, 2003, dtype=np.uint64)
@@ -243,7 +353,7 @@ def main():
             stride = max(1, (W * H) // nsub)
             sub = np.arange(0, W * H, stride, dtype=np.uint64)
             t = time.perf_counter()
-            ref = sc.render(vi[:16], pi, W, H, subset=sub, threads=threads)
+            ref = sc.render(vi[:16], pi, W, H, subset=sub, threads=threads, margin=True)
             dt = time.perf_counter() - t
             # and on one core, a strided sample sized for ~3 s
             n1 = int(min(W * H, max(256, rate / threads * 3.0)))
@@ -255,10 +365,20 @@ def main():
                    "sample": f"{len(sub)} rays (every {stride}th pixel of view 0), oracle analytic-proxy literal "
                              f"ray-march, {dt:.1f} s on {threads} threads",
                    "value_1core": round(len(sub1) / dt1 / 1e6, 6),
-                   "sample_1core": f"{len(sub1)} rays (strided over view 0), {dt1:.1f} s on 1 thread"}
+                   "sample_1core": f"{len(sub1)} rays (strided over view 0), {dt1:.1f} s on 1 thread",
+                   "node": {"nproc": host["nproc"], "cpu_model": host["model"], "affinity_cpus": host["affinity"],
+                            "cgroup_quota_cpus": host["cgroup_quota_cpus"], "omp_num_threads": host["omp_num_threads"],
+                            "threads_used": "the job's CPU share: min(affinity, cgroup quota, OMP_NUM_THREADS)"}}
             img = r.render(vi[:16], pi, W, H, 1, params=params, rgba32f=True, rgba8=True)
             got = img["rgba8"].reshape(-1, 4)[sub.astype(np.int64)]
             psnr = gv.psnr_rgb(got, gv.quantize_rgba8(ref["rgba32f"]))
+            gotf = img["rgba32f"].reshape(-1, 4)[sub.astype(np.int64)]
+            amb = O.ambiguous(ref["margin"])
+            d = np.abs(gotf[:, :3] - ref["rgba32f"][:, :3]).max(axis=1)
+            cpu["parity"] = {"rays": int(len(sub)), "on_threshold": int(amb.sum()),
+                             "max_abs_diff_off_threshold": float(d[~amb].max()) if (~amb).any() else 0.0,
+                             "frac_beyond_1e-4_off_threshold": float((d[~amb] > 1e-4).mean()) if (~amb).any() else 0.0,
+                             "frac_beyond_1e-4_all": float((d > 1e-4).mean())}
 
         result = {
             "metric": "Mrays/s + fps @1920x1080, 1M Gaussians; PSNR vs Vulkan reference",
@@ -279,12 +399,13 @@ def main():
                                    f"ray-query variant, {args.mode} k-buffer",
                        "gaussians": n_input, "survivors": m, "width": W, "height": H,
                        "views": views, "split": args.split, "parallelism": f"{args.split}{world}",
-                       "build": ("quality: host binned-SAH tree + SAH-optimal 4-wide collapse" if args.build == "quality"
+                       "build": ("quality: binned-SAH tree + SAH-optimal 4-wide collapse" if args.build == "quality"
                                  else "fast: device LBVH + greedy 4-wide collapse")},
             "fps": round(1e3 / ms_per_step, 2),
             "kernel_ms": round(kern_avg, 4),
             "kernel_mrays": round(rays_per_rank / (kern_avg * 1e-3) / 1e6, 3) if kern_avg == kern_avg else None,
             "psnr_vs_oracle_db": None if psnr is None else (round(psnr, 2) if math.isfinite(psnr) else "inf"),
+            "frame_sha1": digest,
             "enclose_ms": round(st0["enclose_ms"], 3),
             "accel_ms": round(st0["accel_ms"], 3),
             "first_build_ms": round(first_build["enclose_ms"] + first_build["accel_ms"], 3),

@@ -568,8 +568,9 @@ static thread_local std::vector<float>* g_trace = nullptr;
 //   [1] relative t gap |t_i - t_j| / |t_i| between consecutive accepted crossings (their composite
 //       order);
 //   [2] relative t gap at a boundary: the first crossing of a round (if accepted) against the last one of
-//       the round before, the last slot of a full buffer against the nearest crossing left out, the
-//       crossing that ends the ray (T <= minTransmittance) against its successor, a ray grazing a proxy
+//       the round before, the last slot of a full buffer against the nearest crossing left out (one of the
+//       two accepted), the crossing that ends the ray (T <= minTransmittance) against its successor (if that
+//       one would be accepted), a ray grazing a proxy
 //       whose crossings would be accepted (relative chord |tout - tin| / |t|), and 0 for a crossing
 //       dropped because its t tied bitwise with `last` (the exclusive-tmin round boundary, Q13).
 struct OracleScene {
@@ -690,7 +691,7 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
             ++rounds;
             const float tmin = last + EPS_T, tmax = tmaxb + EPS_T;
             for (uint32_t i = 0; i < MAX_HIT_PER_TRACE; ++i) kb[i] = Hit{INVALID_PARTICLE_ID, INFINITE_DISTANCE};
-            float t_out = INFINITE_DISTANCE;
+            Hit h_out{INVALID_PARTICLE_ID, INFINITE_DISTANCE};  // nearest crossing left out of a full buffer
             // ---- trace(): driver traversal + any-hit (anyhit.rahit:40-71)
             auto anyhit = [&](uint32_t pid, float t) {
                 const bool inRange = (P->tmin_inclusive ? t >= tmin : t > tmin) && t <= tmax;
@@ -711,7 +712,7 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                     }
                 }
                 // out_margin: the nearest crossing left out of (or pushed out of) the full buffer
-                if (hit.id != INVALID_PARTICLE_ID) t_out = std::min(t_out, hit.t);
+                if (hit.id != INVALID_PARTICLE_ID && hit.t < h_out.t) h_out = hit;
             };
             stack.clear();
             stack.push_back(0);
@@ -780,8 +781,15 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
             auto gap = [](float a, float b) { return std::fabs(a - b) / std::max(std::fabs(a), 1e-30f); };
             // out_margin: a crossing tied with the buffer's last slot may or may not make this round,
             // depending on arrival order
-            if (out_margin && kb[MAX_HIT_PER_TRACE - 1].id != INVALID_PARTICLE_ID && t_out < INFINITE_DISTANCE)
-                m_b = std::min(m_b, gap(kb[MAX_HIT_PER_TRACE - 1].t, t_out));
+            auto accepted = [&](uint32_t id) {
+                const HitEval he = evalResponse(s, id, o, d);
+                return he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min;
+            };
+            // (which of two tied crossings makes the round changes the image only if one of them is accepted)
+            if (out_margin && kb[MAX_HIT_PER_TRACE - 1].id != INVALID_PARTICLE_ID && h_out.id != INVALID_PARTICLE_ID &&
+                gap(kb[MAX_HIT_PER_TRACE - 1].t, h_out.t) < 1e-4f &&
+                (accepted(kb[MAX_HIT_PER_TRACE - 1].id) || accepted(h_out.id)))
+                m_b = std::min(m_b, gap(kb[MAX_HIT_PER_TRACE - 1].t, h_out.t));
             round_start = true;
             // ---- process k hits
             for (uint32_t i = 0; i < MAX_HIT_PER_TRACE; ++i) {
@@ -809,11 +817,12 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                         if (h.t >= last) last_ids.push_back(h.id);
                         // the crossing that ends the ray against its successor: a tie decides which of
                         // the two is composited
+                        // (only an accepted successor changes the image by coming first)
                         if (acc && !(st.T > P->min_transmittance)) {
-                            const float tn = i + 1 < MAX_HIT_PER_TRACE && kb[i + 1].id != INVALID_PARTICLE_ID
-                                                 ? kb[i + 1].t
-                                                 : t_out;
-                            if (tn < INFINITE_DISTANCE) m_b = std::min(m_b, gap(h.t, tn));
+                            const Hit nx = i + 1 < MAX_HIT_PER_TRACE && kb[i + 1].id != INVALID_PARTICLE_ID ? kb[i + 1]
+                                                                                                          : h_out;
+                            if (nx.id != INVALID_PARTICLE_ID && gap(h.t, nx.t) < 1e-4f && accepted(nx.id))
+                                m_b = std::min(m_b, gap(h.t, nx.t));
                         }
                     }
                     last = std::max(last, h.t);

@@ -76,3 +76,103 @@ def test_tile_assignment_disjoint_and_complete(gv):
         assert len(keys) == len(allt) == ((W + 7) // 8) * ((H + 7) // 8) * ncams
         sizes = [len(t) for t in tl]
         assert max(sizes) - min(sizes) <= 64  # one 64x64 block at most
+
+
+# ---------------------------------------------------------------- the exchange bench.py runs (dist.FrameExchange)
+def frame_pattern(k, width, height, views=1):
+    y, x = np.mgrid[0:height, 0:width]
+    return np.stack([np.stack([(x + 3 * k + 11 * v) % 251, (y + 5 * k) % 253, (x * 7 + y * 3 + v) % 255,
+                               np.full_like(x, k % 256)], -1) for v in range(views)]).astype(np.uint8)
+
+
+def _exchange_worker(rank, world, port, split, width, height, views, nframes, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    d = importlib.import_module("3dgvrt_lightfield_amd.dist")
+    counter = [0]
+    if split == "tiles":
+        all_tiles = d.rank_tiles(width, height, 1, world, block=2)
+        sizes, item = [t.shape[0] * 64 for t in all_tiles], (4,)
+    else:
+        all_views = d.rank_views(views, world)
+        sizes, item = [len(v) for v in all_views], (height, width, 4)
+    got = {}
+
+    def render(buf):  # frame k's part of this rank, as the GPU renderer would write it
+        k = counter[0]
+        counter[0] += 1
+        img = frame_pattern(k, width, height, views)
+        if split == "tiles":
+            lane = np.arange(64)
+            out = np.zeros((buf.shape[0], 4), np.uint8)
+            for i, (tx, ty, cam, _) in enumerate(all_tiles[rank].astype(np.int64)):
+                px, py = tx * 8 + (lane & 7), ty * 8 + (lane >> 3)
+                ok = (px < width) & (py < height)
+                out[i * 64 + lane[ok]] = img[0, py[ok], px[ok]]
+        else:
+            out = img[all_views[rank]]
+        buf.copy_(torch.from_numpy(out))
+
+    def assemble(parts, k):
+        if split == "tiles":
+            frame = np.zeros((1, height, width, 4), np.uint8)
+            for p, t in zip(parts, all_tiles):
+                d.unpack_tiles_host(p.numpy(), t, width, height, 1, frame)
+        else:
+            frame = np.zeros((views, height, width, 4), np.uint8)
+            for p, vs in zip(parts, all_views):
+                frame[vs] = p.numpy()
+        got[k] = frame
+
+    ex = d.FrameExchange(dist, rank, world, sizes, item, torch.uint8, "cpu", nbuf=2, assemble=assemble)
+    for _ in range(nframes):
+        ex.step(render)
+    ex.drain()
+    if rank == 0:
+        q.put({k: v.copy() for k, v in got.items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,split,width,height,views", [(2, "tiles", 100, 60, 1), (3, "tiles", 37, 29, 1),
+                                                             (2, "views", 24, 16, 5), (3, "views", 16, 8, 3)])
+def test_frame_exchange_double_buffered(world, split, width, height, views):
+    """bench.py's N-rank path on CPU: dist.FrameExchange with two send buffers in flight, unequal parts padded
+    for the gather (tiles: ragged block counts; views: 5 views over 2 ranks), rank-0 assembly per frame.
+    Every frame arrives, in order, equal to the 1-rank frame."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    nframes = 5
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, split, width, height, views, nframes, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    assert sorted(got) == list(range(nframes))
+    for k in range(nframes):
+        np.testing.assert_array_equal(got[k], frame_pattern(k, width, height, views))
+
+
+def test_launch_ranks_gives_n_processes():
+    """`script --gpus 2` started as ONE process comes back as 2 ranks (dist.launch_ranks, bench.py's launcher);
+    a job whose WORLD_SIZE disagrees with --gpus is refused."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    probe = os.path.join(root, "tests", "dist_probe.py")
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    for n in (1, 2, 3):
+        r = subprocess.run([sys.executable, probe, "--gpus", str(n)], capture_output=True, text=True, timeout=240,
+                           env=env)
+        assert r.returncode == 0, r.stderr[-2000:]
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        assert len(line) == 1, r.stdout
+        assert json.loads(line[0]) == {"n_gpus": n, "gpus_arg": n}
+    r = subprocess.run([sys.executable, probe, "--gpus", "2"], capture_output=True, text=True, timeout=120,
+                       env=dict(env, WORLD_SIZE="3", RANK="0"))
+    assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr

@@ -88,3 +88,25 @@ def test_lightfield_grid_16_views(gv, O):
     assert np.abs(img[0] - img[15]).max() > 0.01
     _, sub, ref = _oracle_subset(O, splats, vi, pi, W, H, ncams=ncams, stride=15013)
     _cmp_images(img.reshape(-1, 4)[sub.astype(np.int64)], ref)
+
+
+def test_dense_standin(gv, O):
+    """The dense stand-in (scene.dense_standin: ~150 crossings, ~79 accepted, ~10 LITERAL rounds per ray):
+    FAST and LITERAL vs the oracle on a strided subset, LITERAL counters vs the oracle's on that subset."""
+    splats, W, H, _ = _scene(gv, "dense")
+    vi, pi = gv.scene.mipnerf_camera(W, H)
+    with gv.Renderer(0) as r:
+        m = r.prepare(splats)
+        fast = r.render(vi, pi, W, H, hit_counts=True)
+        lit = r.render(vi, pi, W, H, mode=gv.MODE_LITERAL)
+    m_ref, sub, ref = _oracle_subset(O, splats, vi, pi, W, H, stride=2003)
+    assert m_ref == m
+    st = ref["stats"].reshape(-1, 3)
+    assert st[:, 0].mean() > 140, st.mean(axis=0)  # the workload is what it claims to be
+    idx = sub.astype(np.int64)
+    # ~150 crossings and ~10 round boundaries per ray: ~7 % of the rays carry a decision within the
+    # on-threshold margins (measured on this subset); every other ray must match as everywhere else
+    _cmp_images(fast["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.10)
+    _cmp_images(lit["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.10)
+    amb = O.ambiguous(ref["margin"])
+    assert (fast["hit_counts"].reshape(-1)[idx] != st[:, 1])[~amb].sum() == 0
