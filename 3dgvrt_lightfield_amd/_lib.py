@@ -114,6 +114,7 @@ SIGNATURES = {
     "gvrt_set_stats": (C.c_int32, [H, C.c_int]),
     "gvrt_get_device_properties": (C.c_int32, [C.c_int, _P(DeviceProperties)]),
     "gvrt_get_device_buffers": (C.c_int32, [H, _P(DeviceBuffers)]),
+    "gvrt_read_accel": (C.c_int32, [H, C.c_int, C.c_void_p, C.c_uint64, _P(C.c_uint64)]),
     "gvrt_get_stats": (C.c_int32, [H, _P(Stats)]),
     "gvrt_unpack_tiles_rgba8": (C.c_int32, [H, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
                                             C.c_uint32, C.c_void_p]),

@@ -240,7 +240,9 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
     gvrt_default_accel_params(&d);
     if (!p) p = &d;
     if (p->split_cells > 1023) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "split_cells must be <= 1023");
-    if (p->builder > 2) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "builder must be 0 (LBVH), 1 (PLOC) or 2 (binned SAH, host)");
+    if (p->builder > 3)
+        return gvrt_fail(c, GVRT_ERR_INVALID_ARG,
+                         "builder must be 0 (LBVH), 1 (PLOC), 2 (binned SAH, device) or 3 (binned SAH, host)");
     if (p->collapse > 1) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "collapse must be 0 (greedy) or 1 (SAH-optimal DP)");
     GVRT_HIP(c, hipSetDevice(c->device));
     return gvrt_launch_build_accel(c, *p);
@@ -266,6 +268,22 @@ gvrt_status gvrt_get_device_properties(int device, gvrt_device_properties* out) 
     out->total_memory = (uint64_t)prop.totalGlobalMem;
     int drv = 0;
     if (hipDriverGetVersion(&drv) == hipSuccess) out->driver_version = (uint32_t)drv;
+    return GVRT_OK;
+}
+
+gvrt_status gvrt_read_accel(gvrt_handle c, int which, void* out, uint64_t cap, uint64_t* count) {
+    if (!c || !count) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL argument");
+    if (which != 0 && which != 1) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "which must be 0 (binary) or 1 (4-wide)");
+    if (!c->accel) return gvrt_fail(c, GVRT_ERR_STATE, "gvrt_build_accel has not been called");
+    const uint64_t n = which == 0 ? (c->n_leaves > 1 ? c->n_leaves - 1 : 0) : c->n_nodes4;
+    const void* src = which == 0 ? (const void*)c->d_nodes : (const void*)c->d_nodes4;
+    const uint64_t sz = which == 0 ? sizeof(gvrt::BvhNode) : sizeof(gvrt::Bvh4Node);
+    *count = n;
+    if (!out || !n) return GVRT_OK;
+    if (!src) return gvrt_fail(c, GVRT_ERR_STATE, "tree not kept by this build");
+    GVRT_HIP(c, hipSetDevice(c->device));
+    GVRT_HIP(c, hipMemcpyAsync(out, src, sz * (cap < n ? cap : n), hipMemcpyDeviceToHost, c->stream));
+    GVRT_HIP(c, hipStreamSynchronize(c->stream));
     return GVRT_OK;
 }
 

@@ -95,6 +95,9 @@ gvrt_status gvrt_launch_enclose(gvrt_context* c, const gvrt_enclosing_params* p,
 gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& p);
 gvrt_status gvrt_ploc_build(gvrt_context* c, uint32_t m, const float* leaf_boxes, gvrt::BvhNode* bin,
                             int32_t* leaf_parent, int32_t* node_parent, int32_t* root, uint32_t* iterations);
+// gvrt_sah.hip (the quality build on the device: binned SAH + SAH-optimal collapse)
+gvrt_status gvrt_sah_build_device(gvrt_context* c, uint64_t m, const float* lboxes, gvrt::BvhNode* nodes,
+                                  gvrt::Bvh4Node* out4, uint32_t* depth_out, uint64_t* n4_out, uint32_t* depth4_out);
 // gvrt_render.hip
 gvrt_status gvrt_launch_render_mode(gvrt_context* c, const gvrt::RenderArgs& a, uint64_t nwaves, bool literal);
 gvrt_status gvrt_launch_unpack(gvrt_context* c, const void* packed, const uint32_t* tiles,

@@ -746,6 +746,7 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
             const float ext = ch[a] - cl[a];
             if (!(ext > 0.0f)) continue;
             const float sc = NB / ext;
+            if (!(sc < INFINITY)) continue;  // extent too small to bin
             Box bb[NBMAX];
             uint32_t bn[NBMAX] = {};
             for (int k = 0; k < NB; ++k) bb[k].reset();
@@ -782,7 +783,8 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
         if (best_axis >= 0) {
             axis = best_axis;
             const float sc = NB / (ch[axis] - cl[axis]);
-            const auto it = std::partition(idx.begin() + t.b, idx.begin() + t.e, [&](uint32_t p) {
+            // stable: the device build (gvrt_sah.hip) partitions by a prefix count and must agree
+            const auto it = std::stable_partition(idx.begin() + t.b, idx.begin() + t.e, [&](uint32_t p) {
                 return std::min(NB - 1, (int)((cen[3 * p + axis] - cl[axis]) * sc)) <= best_split;
             });
             mid = (uint32_t)(it - idx.begin());
@@ -845,13 +847,11 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
         });
     for (auto& th : pool) th.join();
     *root = 0;
-    if (keep) {
-        keep->swap(nodes);
-        return GVRT_OK;
-    }
+    // the binary tree also goes to the device (gvrt_read_accel compares it with the device build's)
     GVRT_HIP(c, hipMemcpyAsync(c->d_nodes, nodes.data(), sizeof(BvhNode) * nodes.size(), hipMemcpyHostToDevice,
                                c->stream));
     GVRT_HIP(c, hipStreamSynchronize(c->stream));
+    if (keep) keep->swap(nodes);
     return GVRT_OK;
 }
 
@@ -1257,16 +1257,24 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
         TRYH(hipMemsetAsync(dep, 0, 4, c->stream), "memset");
         const char* be = getenv("GVRT_BUILDER");
         const bool ploc = ap.builder == 1 || (be && be[0] == 'p');  // "ploc": measured 3 % slower to render (more visits), see DESIGN.md
-        const bool sah = !ploc && (ap.builder == 2 || (be && be[0] == 's'));
+        // binned SAH: on the device (builder 2, GVRT_BUILDER=sah), or the same algorithm on the host
+        // (builder 3, GVRT_BUILDER=host: the device build's checker, tests/test_gpu_sah.py)
+        const bool sah_host = !ploc && (ap.builder == 3 || (be && be[0] == 'h'));
+        const bool sah_dev = !ploc && !sah_host && (ap.builder == 2 || (be && be[0] == 's'));
         const char* ce = getenv("GVRT_COLLAPSE");
         const bool dp = (ap.collapse == 1 || (ce && ce[0] == 'd')) && BVH_W == 4;
         std::vector<BvhNode> htree;  // SAH tree kept on the host for the DP collapse
         int32_t root = 0;
+        uint32_t sah_depth = 0, sah_d4 = 0;
+        uint64_t sah_n4 = 0;
         if (ploc) {
             uint32_t iters = 0;
             TRY(gvrt_ploc_build(c, (uint32_t)m, lboxes, c->d_nodes, lpar, npar, &root, &iters));
-        } else if (sah) {
+        } else if (sah_host) {
             TRY(host_sah_build(c, (uint64_t)m, lboxes, &root, dp ? &htree : nullptr));
+        } else if (sah_dev) {
+            TRY(gvrt_sah_build_device(c, (uint64_t)m, lboxes, c->d_nodes, dp ? c->d_nodes4 : nullptr, &sah_depth,
+                                      &sah_n4, &sah_d4));
         } else {
             // leaf-range union table, then the hierarchy with its child boxes in one pass (no refit)
             hlv[0] = lboxes;
@@ -1284,9 +1292,13 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
         }
         const int64_t ni = m - 1;
         // the even-depth rule needs the Karras layout and 4-wide nodes
-        const bool greedy = ploc || sah || BVH_W != 4 || GVRT_NODE64 || !(ce && ce[0] == '0');
+        const bool greedy = ploc || sah_host || sah_dev || BVH_W != 4 || GVRT_NODE64 || !(ce && ce[0] == '0');
         TRYH(hipGetLastError(), "k_karras");
-        if (dp) {
+        if (dp && sah_dev) {  // collapsed by gvrt_sah_build_device
+            c->depth = sah_depth;
+            c->depth4 = sah_d4;
+            c->n_nodes4 = sah_n4;
+        } else if (dp) {
             uint32_t d2 = 0, d4 = 0;
             uint64_t n4 = 0;
             TRY(host_dp_collapse(c, root, m, &htree, &d2, &d4, &n4));

@@ -146,7 +146,7 @@ int main(int argc, char** argv) {
         gvrt_accel_params ap;
         gvrt_default_accel_params(&ap);
         ap.split_cells = (uint32_t)std::atoi(a.get("split-cells", "0").c_str());
-        if (a.get("build", "fast") == "quality") {  // static-scene build: host binned SAH + SAH-optimal collapse
+        if (a.get("build", "fast") == "quality") {  // static-scene build: device binned SAH + SAH-optimal collapse
             ap.builder = 2;
             ap.collapse = 1;
         }

@@ -215,6 +215,17 @@ class Renderer:
         check(lib().gvrt_unpack_tiles_rgba8(self.h, packed_ptr, _lib.vptr(t), nt, width, height, ncams, frame_ptr),
               self.h)
 
+    def read_accel(self, which=1):
+        """gvrt_read_accel: the binary tree (which=0, float32 [n, 16] rows: child boxes, then c0, c1, axis
+        as int32 views) or the 4-wide tree (which=1, [n, 32] rows), as raw 32-bit words (uint32)."""
+        n = C.c_uint64(0)
+        check(lib().gvrt_read_accel(self.h, int(which), None, 0, C.byref(n)), self.h)
+        words = 16 if which == 0 else 32
+        out = np.zeros((int(n.value), words), np.uint32)
+        if n.value:
+            check(lib().gvrt_read_accel(self.h, int(which), out.ctypes.data, n.value, C.byref(n)), self.h)
+        return out
+
     def device_buffers(self):
         """gvrt_get_device_buffers: device pointers of Model::Attributes and the enclosing outputs."""
         b = _lib.DeviceBuffers()

@@ -5,8 +5,8 @@ Gaussians; PSNR vs the reference restated by the CPU oracle).
 Workload at N=1: config 2 ("bicycle" stand-in, 1M synthetic Gaussians, seed 1, 1920x1080, orbit
 camera r=4 / elev 20 / fovy 50, ray-query variant).  A step = one Particle Rendering pass over one
 1920x1080 view with the scene, proxies and BVH resident in HBM (enclosing + BVH build are
-one-shot and reported separately; by default the static-scene quality build, `--build fast` for the
-millisecond device LBVH).
+one-shot and reported separately; by default the static-scene quality build on the device (binned SAH +
+SAH-optimal collapse, ~9 ms at 1M), `--build fast` for the ~1.5 ms device LBVH).
 
 Several GPUs: `python bench.py --gpus N` started as one process launches its N ranks
 itself (torch.distributed.run, one process per GPU; dist.launch_ranks); launched by torch.distributed.run
@@ -63,8 +63,8 @@ def parse():
     ap.add_argument("--no-stats", action="store_true", help="skip the LITERAL stats pass (roofline bytes)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes (roofline.traffic, VALU)")
     ap.add_argument("--build", default="quality", choices=["quality", "fast"],
-                    help="quality: binned-SAH tree + SAH-optimal 4-wide collapse (the static-scene build, as "
-                         "the reference's PREFER_FAST_TRACE BLAS); fast: device LBVH + greedy collapse")
+                    help="quality: device binned-SAH tree + SAH-optimal 4-wide collapse (the static-scene build, "
+                         "as the reference's PREFER_FAST_TRACE BLAS); fast: device LBVH + greedy collapse")
     args = ap.parse_args()
     if args.split == "auto":
         args.split = "tiles" if args.config == "truck" else "views"
@@ -399,7 +399,7 @@ def main():
                                    f"ray-query variant, {args.mode} k-buffer",
                        "gaussians": n_input, "survivors": m, "width": W, "height": H,
                        "views": views, "split": args.split, "parallelism": f"{args.split}{world}",
-                       "build": ("quality: binned-SAH tree + SAH-optimal 4-wide collapse" if args.build == "quality"
+                       "build": ("quality: device binned-SAH tree + SAH-optimal 4-wide collapse" if args.build == "quality"
                                  else "fast: device LBVH + greedy 4-wide collapse")},
             "fps": round(1e3 / ms_per_step, 2),
             "kernel_ms": round(kern_avg, 4),

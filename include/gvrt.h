@@ -155,10 +155,11 @@ gvrt_status gvrt_read_enclosing(gvrt_handle h, float* density12, float* sh48, fl
  * the scene's longest axis (the reference uses NUMBER_OF_CELLS_PER_LONGEST_AXIS = 10), every proxy
  * split into one piece per grid cell its box overlaps, each piece admitting only the crossings whose
  * point lies in its cell (so every crossing is found exactly once).  split_cells <= 1023 (0: no
- * split).  builder: 0 Karras LBVH, 1 PLOC, 2 binned SAH (host side; the PREFER_FAST_TRACE-style
- * quality build of a static scene).  collapse: 0 greedy surface-area 4-wide collapse on the
- * device, 1 surface-area-optimal collapse (dynamic programming, host side: ~2.5 % fewer node visits,
- * tens of ms of build time). */
+ * split).  builder: 0 Karras LBVH, 1 PLOC, 2 binned SAH on the device (the PREFER_FAST_TRACE-style
+ * quality build of a static scene, VulkanFullRT.cpp:621), 3 the same binned SAH on the host (the
+ * device build's checker: identical trees).  collapse: 0 greedy surface-area 4-wide collapse on the
+ * device, 1 surface-area-optimal collapse (dynamic programming; on the device with builder 2, on
+ * the host otherwise). */
 typedef struct {
     uint32_t split_cells;
     uint32_t builder;
@@ -172,6 +173,13 @@ void gvrt_default_accel_params(gvrt_accel_params* p);
  * BVH over the proxies (Morton codes, radix sort, Karras hierarchy, 4-wide collapse). */
 gvrt_status gvrt_build_accel(gvrt_handle h);
 gvrt_status gvrt_build_accel_ex(gvrt_handle h, const gvrt_accel_params* p);
+
+/* Copy the acceleration structure to host memory (parity checks of the builders, like inspecting a
+ * serialized VkAccelerationStructure).  which = 0: the binary tree (n_leaves - 1 nodes of 64 B:
+ * child 0 box, child 1 box, c0, c1, split axis, 0); which = 1: the 4-wide tree the render kernel
+ * traverses (128 B per node).  *count receives the node count; at most cap nodes are written (out may
+ * be NULL to query the count). */
+gvrt_status gvrt_read_accel(gvrt_handle h, int which, void* out, uint64_t cap, uint64_t* count);
 
 /* Particle Rendering pass: buildCommandBuffer (VulkanFullRT.cpp:1185-1244) dispatching
  * raygen/anyhit (RT) or particleRendering.comp (RQ), and the light-field launch

@@ -102,7 +102,7 @@ def test_split_tiny_scenes_and_limits(gv, O):
         with pytest.raises(gv.GvrtError):
             r.build_accel(split_cells=1024)
         with pytest.raises(gv.GvrtError):
-            r.build_accel(builder=3)
+            r.build_accel(builder=4)
 
 
 @pytest.mark.parametrize("split", [0, 10])
