@@ -423,6 +423,14 @@ __device__ inline NodeS load_node(const Bvh4Node* __restrict__ p) { return *p; }
 #define NODE_PAD(nd, j) (nd).pad[j]
 #endif
 
+// lane id recomputed at the point of use (asm volatile: not merged with the kernel-entry value, so no
+// register holds it through the traversal)
+__device__ inline int lane_now() {
+    int r;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(r));
+    return r;
+}
+
 __device__ inline uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ inline float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
@@ -467,11 +475,13 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
     __shared__ float s_T[WGW][64];
     __shared__ float s_last[WGW][64];  // `last` and the AABB exit: round-boundary state, not needed in traversal
     __shared__ float s_tmax[WGW][64];
+    __shared__ uint32_t s_pxy[WGW][64];  // px | py << 16, parked for the output stage (not live in VGPRs)
 #if !GVRT_VSTACK
     __shared__ int32_t s_stack[WGW][STACK_DEPTH];
 #endif
-    const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
+    // lane from mbcnt (no register input), wave index uniform
+    const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     // (Round-robin workgroup -> XCD dealing is kept: an XCD-contiguous band remap measured 33 % slower,
     // the bands' very different costs leave a long tail; L2 hit rate is already ~91 %.)
     const uint64_t tile_idx = (uint64_t)blockIdx.x * WGW + wid;  // tile-list position
@@ -536,6 +546,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
     s_tmax[wid][lane] = tmaxb;
     s_acc[wid][lane] = make_float4(0.0f, 0.0f, 0.0f, a.alpha_init);
     s_T[wid][lane] = 1.0f;
+    s_pxy[wid][lane] = px | py << 16;
     // counters: only the STATS instantiation keeps them (registers); the accepted-hit count is
     // recovered exactly from the alpha accumulator (RQ/RT alpha = alpha_init + #accepted, Q10)
     uint32_t nproc = 0, rounds = 0;
@@ -928,12 +939,18 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
         if constexpr (STATS) cyc_comp += __builtin_amdgcn_s_memtime() - t_comp0;
     }
 
-    // ---------------- outputs
-    const float4 acc = s_acc[wid][lane];
+    // ---------------- outputs (pixel coordinates and lane recomputed: kept live through the traversal
+    // they were spilled to scratch)
+    const int olane = lane_now();
+    const float4 acc = s_acc[wid][olane];
     const float cr = acc.x, cg = acc.y, cb = acc.z, calpha = acc.w;
-    if (valid) {
-        const uint64_t pix = ((uint64_t)cam * a.height + py) * a.width + px;
-        const uint64_t oi = a.packed ? tile_idx * 64 + lane : pix;
+    const uint32_t pxy = s_pxy[wid][olane];
+    const uint32_t opx = pxy & 0xFFFFu, opy = pxy >> 16;
+    const bool ovalid = opx < a.width && opy < a.height && cam < a.ncams;
+    const uint64_t otile = (uint64_t)blockIdx.x * WGW + (uint32_t)wid;
+    if (ovalid) {
+        const uint64_t pix = ((uint64_t)cam * a.height + opy) * a.width + opx;
+        const uint64_t oi = a.packed ? otile * 64 + olane : pix;
         if (rgba32f_) reinterpret_cast<float4*>(rgba32f_)[oi] = make_float4(cr, cg, cb, calpha);
         if (rgba8_) {
             auto q8 = [](float f) -> uint32_t { return (uint32_t)(fminf(fmaxf(f, 0.0f), 1.0f) * 255.0f + 0.5f); };
@@ -942,18 +959,18 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
         if (hit_counts_) hit_counts_[oi] = (uint32_t)(calpha - a.alpha_init);
         if (ray_dirs_) {
             const uint64_t di = a.ray_dirs_layout == 1
-                                    ? ((uint64_t)cam * a.width * a.height + (uint64_t)px * a.height + py)
+                                    ? ((uint64_t)cam * a.width * a.height + (uint64_t)opx * a.height + opy)
                                     : pix;
             reinterpret_cast<float4*>(ray_dirs_)[di] = make_float4(d.x, d.y, d.z, 0.0f);
         }
     } else if (a.packed) {
-        const uint64_t oi = tile_idx * 64 + lane;
+        const uint64_t oi = otile * 64 + olane;
         if (rgba32f_) reinterpret_cast<float4*>(rgba32f_)[oi] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (rgba8_) reinterpret_cast<uint32_t*>(rgba8_)[oi] = 0u;
         if (hit_counts_) hit_counts_[oi] = 0u;
     }
     if constexpr (STATS) {
-        unsigned long long s0 = nproc, s1 = valid ? (uint32_t)(calpha - a.alpha_init) : 0u, s2 = rounds, s5 = l_leaves;
+        unsigned long long s0 = nproc, s1 = ovalid ? (uint32_t)(calpha - a.alpha_init) : 0u, s2 = rounds, s5 = l_leaves;
         for (int off = 32; off > 0; off >>= 1) {
             s0 += __shfl_xor(s0, off);
             s1 += __shfl_xor(s1, off);
