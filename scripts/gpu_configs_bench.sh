@@ -2,17 +2,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/configs
-for cfg in bicycle garden truck lightfield; do
+for cfg in ${CFGS:-bicycle garden truck lightfield dense}; do
   timeout -k 10 300 python bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/configs/$cfg.json 2> gpurun_out/configs/$cfg.err || { echo "$cfg failed"; tail -5 gpurun_out/configs/$cfg.err; exit 1; }
   python3 -c "import json; d=json.load(open('gpurun_out/configs/$cfg.json')); print('$cfg', d['value'], d['unit'], d['ms_per_step'], 'ms/step', d['kernel_ms'], 'kernel ms', d['roofline']['frac'], 'frac', d['enclose_ms'], d['accel_ms'], d['config']['width'], d['config']['height'], d['config']['views'], d['config']['survivors'])"
 done
-timeout -k 10 300 python -c "
-import importlib, sys, time
-sys.path.insert(0, '.')
-gv = importlib.import_module('3dgvrt_lightfield_amd')
-s = gv.scene.mipnerf_standin(1_000_000, seed=1)
-with gv.Renderer(0) as r:
-    for col in (0, 1, 0, 1):
-        r.prepare(s, collapse=col)
-        print('collapse', col, 'accel_ms', round(r.stats()['accel_ms'], 2))
-" > gpurun_out/configs/collapse.txt 2>&1; cat gpurun_out/configs/collapse.txt
