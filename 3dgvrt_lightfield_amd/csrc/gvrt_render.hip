@@ -5,8 +5,8 @@
 // raygenGaussianLightField.rgen:114-202 (multi-camera light field), and the driver's BVH
 // traversal behind traceRayEXT / rayQueryProceedEXT.
 //
-// Mapping to CDNA4: one wave64 = one 8x8 pixel tile (one lane per ray), four tiles per
-// 256-thread workgroup.  Traversal is wave-uniform (packet traversal) over the 4-wide collapse of
+// Mapping to CDNA4: one wave64 = one 8x8 pixel tile (one lane per ray), one wave per workgroup, tiles
+// dispatched in 8x4 supertiles.  Traversal is wave-uniform (packet traversal) over the 4-wide collapse of
 // the LBVH: node and leaf records are addressed by a wave-uniform index and fetched with scalar
 // loads (two s_load_dwordx16 per 128-B node, one per 64-B record), every lane clips its own ray
 // against the four child boxes, and ballots decide which children the packet descends into; the
