@@ -24,6 +24,7 @@ constexpr float IPHI = 0.618033988749895f;
 constexpr float ICOSA_VRT_SCALE = 0.5f * 1.323169076499215f;  // particlePrimitives.comp:78-79
 constexpr float SQRT3 = 1.7320508075688772f;
 constexpr int STACK_DEPTH = 128;                      // per-wave LDS traversal stack
+constexpr int TILE_BUCKETS = 64;                      // cost classes of the cost-ordered dispatch (4 per octave)
 
 struct alignas(16) RenderRec {
     float px, py, pz, density;
@@ -130,6 +131,8 @@ struct RenderArgs {
     float* ray_dirs;
     uint32_t* hit_counts;
     unsigned long long* stats;  // [crossings, accepted, rounds] or null
+    uint8_t* tile_bucket;       // per tile (cam, ty, tx row-major): log-scale cost class of its wave, or null
+    uint32_t* tile_hist;        // tiles per cost class (TILE_BUCKETS), for the next frame's order
 };
 
 // kernelScale, particlePrimitives.comp:81-105

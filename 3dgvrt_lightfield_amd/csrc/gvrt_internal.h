@@ -72,6 +72,14 @@ struct gvrt_context {
     uint32_t async_pending = 0;
     double async_ms_sum = 0.0;         // kernel times of async launches drained before the next gvrt_sync
     uint64_t async_drained = 0;
+    // cost-ordered dispatch: the previous launch's per-tile cost classes, tiles ordered costliest first
+    uint64_t ord_key = 0;            // width | height << 16 | ncams << 32 of the arrays below
+    uint64_t ord_n = 0;              // tiles
+    bool ord_ready = false;          // d_order holds an order for ord_key
+    uint8_t* d_tbucket = nullptr;    // per tile: cost class of the last launch
+    uint32_t* d_thist = nullptr;     // tiles per cost class (zero between launches)
+    uint32_t* d_tcode = nullptr;     // per tile: packed tile code (cam << 24 | ty << 12 | tx)
+    uint32_t* d_order = nullptr;     // tile codes, costliest class first
     void* d_stage = nullptr;  // staging for host outputs
     uint64_t stage_cap = 0;
 
@@ -100,5 +108,6 @@ gvrt_status gvrt_sah_build_device(gvrt_context* c, uint64_t m, const float* lbox
                                   gvrt::Bvh4Node* out4, uint32_t* depth_out, uint64_t* n4_out, uint32_t* depth4_out);
 // gvrt_render.hip
 gvrt_status gvrt_launch_render_mode(gvrt_context* c, const gvrt::RenderArgs& a, uint64_t nwaves, bool literal);
+gvrt_status gvrt_launch_tile_order(gvrt_context* c);
 gvrt_status gvrt_launch_unpack(gvrt_context* c, const void* packed, const uint32_t* tiles,
                                uint64_t ntiles, uint32_t width, uint32_t height, void* frame);

@@ -450,6 +450,9 @@ __device__ inline float unif(float v) { return __int_as_float(__builtin_amdgcn_r
 // Dispatch order: workgroups walk 8 x 4-block supertiles (64 x 32 px with one-wave workgroups) in row-major
 // order, so the tiles in flight form a compact band: 0.9 / 2.0 / 1.8 % faster than row-major on bicycle /
 // dense / garden (4 x 4: mixed, 16 x 8: within noise).
+#ifndef GVRT_EXP_TILECOST
+#define GVRT_EXP_TILECOST 0
+#endif
 #ifndef GVRT_ST_W
 #define GVRT_ST_W 8
 #endif
@@ -488,6 +491,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
     __shared__ float s_last[WGW][64];  // `last` and the AABB exit: round-boundary state, not needed in traversal
     __shared__ float s_tmax[WGW][64];
     __shared__ uint32_t s_pxy[WGW][64];  // px | py << 16, parked for the output stage (not live in VGPRs)
+    __shared__ unsigned long long s_t0[WGW];  // wave start (s_memtime), for the per-tile cost class
 #if !GVRT_VSTACK
     __shared__ int32_t s_stack[WGW][STACK_DEPTH];
 #endif
@@ -510,8 +514,9 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
         const uint32_t bx_n = (a.tiles_x + WG_TW - 1) / WG_TW, by_n = (a.tiles_y + WG_TH - 1) / WG_TH;
         const uint32_t sx_n = (bx_n + ST_W - 1) / ST_W, sy_n = (by_n + ST_H - 1) / ST_H;
         const uint64_t per = (uint64_t)sx_n * sy_n * (ST_W * ST_H);
-        cam = (uint32_t)(blockIdx.x / per);
-        const uint32_t rem = (uint32_t)(blockIdx.x % per);
+        const uint64_t bid = blockIdx.x;
+        cam = (uint32_t)(bid / per);
+        const uint32_t rem = (uint32_t)(bid % per);
         const uint32_t st = rem / (ST_W * ST_H), in = rem % (ST_W * ST_H);
         const uint32_t by = (st / sx_n) * ST_H + in / ST_W, bx = (st % sx_n) * ST_W + in % ST_W;
         ty = by * WG_TH + (uint32_t)wid / WG_TW;
@@ -521,6 +526,9 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
     cam = uni(cam);
     const uint32_t px = tx * 8 + (lane & 7), py = ty * 8 + (lane >> 3);
     const bool valid = px < a.width && py < a.height && cam < a.ncams;
+#if GVRT_EXP_TILECOST  // timing probe: the hit-count output receives the wave's cycles
+    const uint64_t exp_t0 = __builtin_amdgcn_s_memtime();
+#endif
 #if GVRT_TRACE
     const bool trace_on = valid && ((uint64_t)cam * a.height + py) * a.width + px == g_trace_pix;
 #endif
@@ -563,6 +571,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
     s_acc[wid][lane] = make_float4(0.0f, 0.0f, 0.0f, a.alpha_init);
     s_T[wid][lane] = 1.0f;
     s_pxy[wid][lane] = px | py << 16;
+    if (a.tile_bucket) s_t0[wid] = __builtin_amdgcn_s_memtime();
     // counters: only the STATS instantiation keeps them (registers); the accepted-hit count is
     // recovered exactly from the alpha accumulator (RQ/RT alpha = alpha_init + #accepted, Q10)
     uint32_t nproc = 0, rounds = 0;
@@ -972,7 +981,11 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
             auto q8 = [](float f) -> uint32_t { return (uint32_t)(fminf(fmaxf(f, 0.0f), 1.0f) * 255.0f + 0.5f); };
             reinterpret_cast<uint32_t*>(rgba8_)[oi] = q8(cr) | (q8(cg) << 8) | (q8(cb) << 16) | (q8(calpha) << 24);
         }
+#if GVRT_EXP_TILECOST
+        if (hit_counts_) hit_counts_[oi] = (uint32_t)(__builtin_amdgcn_s_memtime() - exp_t0);
+#else
         if (hit_counts_) hit_counts_[oi] = (uint32_t)(calpha - a.alpha_init);
+#endif
         if (ray_dirs_) {
             const uint64_t di = a.ray_dirs_layout == 1
                                     ? ((uint64_t)cam * a.width * a.height + (uint64_t)opx * a.height + opy)
@@ -984,6 +997,16 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
         if (rgba32f_) reinterpret_cast<float4*>(rgba32f_)[oi] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (rgba8_) reinterpret_cast<uint32_t*>(rgba8_)[oi] = 0u;
         if (hit_counts_) hit_counts_[oi] = 0u;
+    }
+    if (a.tile_bucket && olane == 0) {
+        // this tile's cost class, 4 per octave of its cycles (vector stores / atomics from lane 0); tile
+        // coordinates from lane 0's pixel
+        const uint64_t cyc = __builtin_amdgcn_s_memtime() - s_t0[wid];
+        const float lc = 4.0f * __log2f((float)cyc + 1.0f) - 40.0f;  // 1 k cycles: class 0
+        const uint32_t b = (uint32_t)fminf(fmaxf(lc, 0.0f), (float)(TILE_BUCKETS - 1));
+        const uint32_t tid = (cam * a.tiles_y + (opy >> 3)) * a.tiles_x + (opx >> 3);
+        a.tile_bucket[tid] = (uint8_t)b;
+        atomicAdd(a.tile_hist + b, 1u);
     }
     if constexpr (STATS) {
         unsigned long long s0 = nproc, s1 = ovalid ? (uint32_t)(calpha - a.alpha_init) : 0u, s2 = rounds, s5 = l_leaves;
@@ -1091,6 +1114,36 @@ extern "C" int gvrt_debug_trace_get(float* out, int maxn) {
     return (int)n;
 }
 #endif
+
+// The next launch's tile order from this launch's cost classes: one workgroup counts each class's start
+// (costliest class first), scatters the tile codes with LDS atomics and clears the class counts for the
+// next launch.  Order within a class is arbitrary (it changes only which wave renders a tile when).
+__global__ __launch_bounds__(1024) void k_tile_order(uint32_t n, const uint8_t* __restrict__ bucket,
+                                                     const uint32_t* __restrict__ code, uint32_t* __restrict__ hist,
+                                                     uint32_t* __restrict__ order) {
+    __shared__ uint32_t base[TILE_BUCKETS];
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int b = TILE_BUCKETS - 1; b >= 0; --b) {
+            base[b] = acc;
+            acc += hist[b];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < TILE_BUCKETS) hist[threadIdx.x] = 0u;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t pos = atomicAdd(&base[bucket[i]], 1u);
+        if (pos < n) order[pos] = code[i];
+    }
+}
+
+gvrt_status gvrt_launch_tile_order(gvrt_context* c) {
+    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, c->stream, (uint32_t)c->ord_n, c->d_tbucket, c->d_tcode,
+                       c->d_thist, c->d_order);
+    GVRT_HIP(c, hipGetLastError());
+    c->ord_ready = true;
+    return GVRT_OK;
+}
 
 gvrt_status gvrt_launch_unpack(gvrt_context* c, const void* packed, const uint32_t* tiles, uint64_t ntiles,
                                uint32_t width, uint32_t height, void* frame) {

@@ -145,3 +145,38 @@ def test_unpack_tiles_rejects_tiles_outside_the_frame(gv, config1):
         with pytest.raises(ValueError):  # short camera arrays are refused on the host side
             vi, pi = gv.scene.config1_camera(W, H)
             r.render_device(vi, pi, W, H, ncams=2, rgba8_ptr=frame.data_ptr())
+
+
+def test_cost_ordered_dispatch_changes_no_pixel(gv, config1):
+    """Cost-ordered dispatch (gvrt_api.hip: each launch records its tiles' cost classes, the next launch of the
+    same frame size takes the tiles costliest first): the first launch (default order), the ordered ones after
+    it, launches after a frame-size change, a multi-camera launch, and a tile-list launch (which keeps the
+    caller's order) all give the same pixels, rgba8, hit counts and ray directions."""
+    W, H = 72, 40  # 9 x 5 tiles
+    vi, pi = gv.scene.config1_camera(W, H)
+    with gv.Renderer(0) as r:
+        r.prepare(config1)
+        kw = dict(hit_counts=True, ray_dirs=True)
+        first = r.render(vi, pi, W, H, **kw)
+        for _ in range(3):
+            again = r.render(vi, pi, W, H, **kw)
+            for k in ("rgba32f", "rgba8", "hit_counts", "ray_dirs"):
+                np.testing.assert_array_equal(again[k], first[k])
+        other = r.render(vi, pi, 33, 17)  # a new frame size restarts from the default order
+        np.testing.assert_array_equal(r.render(vi, pi, 33, 17)["rgba32f"], other["rgba32f"])
+        np.testing.assert_array_equal(r.render(vi, pi, W, H)["rgba32f"], first["rgba32f"])
+        # three cameras in one launch vs each alone
+        vi3, pi3 = gv.camera.lightfield_grid_rig((0.0, 0.0, 3.0), (0.0, 0.0, 0.0), nx=3, ny=1, spacing=0.2,
+                                                  aspect=gv.camera.aspect_ratio(W, H))
+        multi = [r.render(vi3, pi3, W, H, ncams=3)["rgba32f"] for _ in range(3)]
+        np.testing.assert_array_equal(multi[1], multi[0])
+        np.testing.assert_array_equal(multi[2], multi[0])
+        for cam in range(3):
+            single = r.render(vi3[16 * cam:16 * (cam + 1)], pi3, W, H)["rgba32f"]
+            np.testing.assert_array_equal(single[0], multi[0][cam])
+        # a tile list keeps the caller's order and covers only its tiles
+        t = np.asarray([(2, 1, 0, 0), (0, 0, 0, 0), (8, 4, 0, 0)], np.uint16)
+        part = r.render(vi, pi, W, H, tiles=t)["rgba32f"][0]
+        for tx, ty, _, _ in t:
+            np.testing.assert_array_equal(part[8 * ty:8 * ty + 8, 8 * tx:8 * tx + 8],
+                                          first["rgba32f"][0][8 * ty:8 * ty + 8, 8 * tx:8 * tx + 8])
