@@ -387,7 +387,7 @@ static gvrt_status ensure_tile_order(gvrt_context* c, uint32_t tiles_x, uint32_t
     const uint64_t n = (uint64_t)tiles_x * tiles_y * ncams;
     gvrt_status s;
     if ((s = gvrt_dalloc(c, (void**)&c->d_tbucket, n))) return s;
-    if ((s = gvrt_dalloc(c, (void**)&c->d_thist, 4 * TILE_BUCKETS))) return s;
+    if ((s = gvrt_dalloc(c, (void**)&c->d_thist, 4 * 4 * TILE_BUCKETS))) return s;
     if ((s = gvrt_dalloc(c, (void**)&c->d_tcode, 4 * n))) return s;
     if ((s = gvrt_dalloc(c, (void**)&c->d_order, 4 * n))) return s;
     std::vector<uint32_t> code(n);
@@ -395,7 +395,8 @@ static gvrt_status ensure_tile_order(gvrt_context* c, uint32_t tiles_x, uint32_t
         for (uint32_t ty = 0; ty < tiles_y; ++ty)
             for (uint32_t tx = 0; tx < tiles_x; ++tx) code[i++] = (cam << 24) | (ty << 12) | tx;
     GVRT_HIP(c, hipMemcpy(c->d_tcode, code.data(), 4 * n, hipMemcpyHostToDevice));
-    GVRT_HIP(c, hipMemset(c->d_thist, 0, 4 * TILE_BUCKETS));
+    GVRT_HIP(c, hipMemset(c->d_thist, 0, 4 * 4 * TILE_BUCKETS));
+    c->ord_parity = 0;
     c->ord_n = n;
     c->ord_key = key;
     return GVRT_OK;
@@ -504,7 +505,7 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         const uint64_t key = (uint64_t)width | ((uint64_t)height << 16) | ((uint64_t)ncams << 32);
         if ((s = ensure_tile_order(c, tiles_x, tiles_y, ncams, key))) return s;
         a.tile_bucket = c->d_tbucket;
-        a.tile_hist = c->d_thist;
+        a.tile_hist = c->d_thist + TILE_BUCKETS * c->ord_parity;
         if (c->ord_ready) a.tiles = c->d_order;  // every tile once, costliest first
     }
     a.ntiles = nwork;

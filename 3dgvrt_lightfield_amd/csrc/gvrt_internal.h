@@ -77,7 +77,8 @@ struct gvrt_context {
     uint64_t ord_n = 0;              // tiles
     bool ord_ready = false;          // d_order holds an order for ord_key
     uint8_t* d_tbucket = nullptr;    // per tile: cost class of the last launch
-    uint32_t* d_thist = nullptr;     // tiles per cost class (zero between launches)
+    uint32_t* d_thist = nullptr;     // [class counts, fill cursors] x launch parity (gvrt_render.hip)
+    uint32_t ord_parity = 0;         // parity of the next launch
     uint32_t* d_tcode = nullptr;     // per tile: packed tile code (cam << 24 | ty << 12 | tx)
     uint32_t* d_order = nullptr;     // tile codes, costliest class first
     void* d_stage = nullptr;  // staging for host outputs

@@ -1115,12 +1115,16 @@ extern "C" int gvrt_debug_trace_get(float* out, int maxn) {
 }
 #endif
 
-// The next launch's tile order from this launch's cost classes: one workgroup counts each class's start
-// (costliest class first), scatters the tile codes with LDS atomics and clears the class counts for the
-// next launch.  Order within a class is arbitrary (it changes only which wave renders a tile when).
-__global__ __launch_bounds__(1024) void k_tile_order(uint32_t n, const uint8_t* __restrict__ bucket,
-                                                     const uint32_t* __restrict__ code, uint32_t* __restrict__ hist,
-                                                     uint32_t* __restrict__ order) {
+// The next launch's tile order from this launch's cost classes, costliest class first.  Class counts and
+// fill cursors are double-buffered by launch parity: the render kernel of launch k counts into hist[k & 1],
+// this kernel turns them into class starts (every block computes the 64-entry prefix), places each tile at
+// start + cursor (ranks within a block by LDS atomics, one global atomic per class per block) and clears the
+// other parity's arrays for launch k + 1.  Order within a class is arbitrary (it
+// changes only which wave renders a tile when).
+__global__ __launch_bounds__(256) void k_tile_order(uint32_t n, const uint8_t* __restrict__ bucket,
+                                                    const uint32_t* __restrict__ code, uint32_t* __restrict__ hist,
+                                                    uint32_t* __restrict__ fill, uint32_t* __restrict__ hist_next,
+                                                    uint32_t* __restrict__ fill_next, uint32_t* __restrict__ order) {
     __shared__ uint32_t base[TILE_BUCKETS];
     if (threadIdx.x == 0) {
         uint32_t acc = 0;
@@ -1129,18 +1133,36 @@ __global__ __launch_bounds__(1024) void k_tile_order(uint32_t n, const uint8_t* 
             acc += hist[b];
         }
     }
+    if (blockIdx.x == 0 && threadIdx.x < TILE_BUCKETS) {
+        hist_next[threadIdx.x] = 0u;
+        fill_next[threadIdx.x] = 0u;
+    }
     __syncthreads();
-    if (threadIdx.x < TILE_BUCKETS) hist[threadIdx.x] = 0u;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint32_t pos = atomicAdd(&base[bucket[i]], 1u);
+    // block-level: ranks within the block's classes by LDS atomics, then one global cursor add per class
+    __shared__ uint32_t cnt[TILE_BUCKETS], off[TILE_BUCKETS];
+    if (threadIdx.x < TILE_BUCKETS) cnt[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t b = i < n ? bucket[i] : 0u;
+    const uint32_t r = i < n ? atomicAdd(&cnt[b], 1u) : 0u;
+    __syncthreads();
+    if (threadIdx.x < TILE_BUCKETS && cnt[threadIdx.x]) off[threadIdx.x] = atomicAdd(fill + threadIdx.x, cnt[threadIdx.x]);
+    __syncthreads();
+    if (i < n) {
+        const uint32_t pos = base[b] + off[b] + r;
         if (pos < n) order[pos] = code[i];
     }
 }
 
 gvrt_status gvrt_launch_tile_order(gvrt_context* c) {
-    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, c->stream, (uint32_t)c->ord_n, c->d_tbucket, c->d_tcode,
-                       c->d_thist, c->d_order);
+    const uint32_t p = c->ord_parity;
+    uint32_t* h = c->d_thist;  // [hist 0, hist 1, fill 0, fill 1] x TILE_BUCKETS
+    const uint32_t n = (uint32_t)c->ord_n;
+    hipLaunchKernelGGL(k_tile_order, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, c->d_tbucket, c->d_tcode,
+                       h + TILE_BUCKETS * p, h + TILE_BUCKETS * (2 + p), h + TILE_BUCKETS * (1 - p),
+                       h + TILE_BUCKETS * (3 - p), c->d_order);
     GVRT_HIP(c, hipGetLastError());
+    c->ord_parity = 1 - p;
     c->ord_ready = true;
     return GVRT_OK;
 }
