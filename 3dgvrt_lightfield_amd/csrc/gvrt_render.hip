@@ -1126,12 +1126,14 @@ __global__ __launch_bounds__(256) void k_tile_order(uint32_t n, const uint8_t* _
                                                     uint32_t* __restrict__ fill, uint32_t* __restrict__ hist_next,
                                                     uint32_t* __restrict__ fill_next, uint32_t* __restrict__ order) {
     __shared__ uint32_t base[TILE_BUCKETS];
+    __shared__ uint32_t total;
     if (threadIdx.x == 0) {
         uint32_t acc = 0;
         for (int b = TILE_BUCKETS - 1; b >= 0; --b) {
             base[b] = acc;
             acc += hist[b];
         }
+        total = acc;
     }
     if (blockIdx.x == 0 && threadIdx.x < TILE_BUCKETS) {
         hist_next[threadIdx.x] = 0u;
@@ -1143,6 +1145,10 @@ __global__ __launch_bounds__(256) void k_tile_order(uint32_t n, const uint8_t* _
     if (threadIdx.x < TILE_BUCKETS) cnt[threadIdx.x] = 0u;
     __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (total != n) {  // counts not from one complete launch (never expected): the plain order, every tile once
+        if (i < n) order[i] = code[i];
+        return;
+    }
     const uint32_t b = i < n ? bucket[i] : 0u;
     const uint32_t r = i < n ? atomicAdd(&cnt[b], 1u) : 0u;
     __syncthreads();
