@@ -6,6 +6,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -374,9 +375,13 @@ static bool tile_order_enabled() {
     return on;
 }
 
+// Arrays of the order for a launch of n tile-list entries: kept while the frame size and the tile list stay
+// the same (list == null: a full frame, whose list is every tile in supertile order), reset otherwise.
 static gvrt_status ensure_tile_order(gvrt_context* c, uint32_t tiles_x, uint32_t tiles_y, uint32_t ncams,
-                                     uint64_t key) {
-    if (c->ord_key == key && c->d_tbucket) return GVRT_OK;
+                                     const std::vector<uint32_t>* list) {
+    const uint64_t key = (uint64_t)tiles_x | ((uint64_t)tiles_y << 16) | ((uint64_t)ncams << 32) |
+                         (list ? 0ull : (1ull << 63));
+    if (c->ord_key == key && c->d_tbucket && (!list || *list == c->ord_list)) return GVRT_OK;
     GVRT_HIP(c, hipStreamSynchronize(c->stream));  // queued launches may still read the old arrays
     gvrt_dfree(c, (void**)&c->d_tbucket);
     gvrt_dfree(c, (void**)&c->d_thist);
@@ -384,17 +389,29 @@ static gvrt_status ensure_tile_order(gvrt_context* c, uint32_t tiles_x, uint32_t
     gvrt_dfree(c, (void**)&c->d_order);
     c->ord_ready = false;
     c->ord_key = 0;
-    const uint64_t n = (uint64_t)tiles_x * tiles_y * ncams;
+    c->ord_list.clear();
+    const uint64_t n = list ? list->size() : (uint64_t)tiles_x * tiles_y * ncams;
+    if (n == 0) return GVRT_OK;
     gvrt_status s;
     if ((s = gvrt_dalloc(c, (void**)&c->d_tbucket, n))) return s;
     if ((s = gvrt_dalloc(c, (void**)&c->d_thist, 4 * 4 * TILE_BUCKETS))) return s;
-    if ((s = gvrt_dalloc(c, (void**)&c->d_tcode, 4 * n))) return s;
     if ((s = gvrt_dalloc(c, (void**)&c->d_order, 4 * n))) return s;
-    std::vector<uint32_t> code(n);
-    for (uint32_t cam = 0, i = 0; cam < ncams; ++cam)
-        for (uint32_t ty = 0; ty < tiles_y; ++ty)
-            for (uint32_t tx = 0; tx < tiles_x; ++tx) code[i++] = (cam << 24) | (ty << 12) | tx;
-    GVRT_HIP(c, hipMemcpy(c->d_tcode, code.data(), 4 * n, hipMemcpyHostToDevice));
+    if (!list) {
+        // the full frame as a tile list in the render kernel's supertile order (its first launch's order)
+        if ((s = gvrt_dalloc(c, (void**)&c->d_tcode, 4 * n))) return s;
+        std::vector<uint32_t> code;
+        code.reserve(n);
+        const uint32_t STW = 8, STH = 4;  // as GVRT_ST_W / GVRT_ST_H of gvrt_render.hip
+        for (uint32_t cam = 0; cam < ncams; ++cam)
+            for (uint32_t sy = 0; sy < tiles_y; sy += STH)
+                for (uint32_t sx = 0; sx < tiles_x; sx += STW)
+                    for (uint32_t ty = sy; ty < std::min(sy + STH, tiles_y); ++ty)
+                        for (uint32_t tx = sx; tx < std::min(sx + STW, tiles_x); ++tx)
+                            code.push_back((cam << 24) | (ty << 12) | tx);
+        GVRT_HIP(c, hipMemcpy(c->d_tcode, code.data(), 4 * n, hipMemcpyHostToDevice));
+    } else {
+        c->ord_list = *list;
+    }
     GVRT_HIP(c, hipMemset(c->d_thist, 0, 4 * 4 * TILE_BUCKETS));
     c->ord_parity = 0;
     c->ord_n = n;
@@ -499,14 +516,15 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         a.tiles = c->d_tiles;
         nwork = ntiles;
     }
-    // cost-ordered dispatch of full frames (a caller's tile list keeps its order: packed outputs follow it)
-    const bool ordered = tile_order_enabled() && !tiles && !out->packed;
+    // cost-ordered dispatch: full frames and caller tile lists alike (the kernel renders list position
+    // perm[i] in workgroup i; outputs stay where the list puts them)
+    const bool ordered = tile_order_enabled() && nwork > 0;
     if (ordered) {
-        const uint64_t key = (uint64_t)width | ((uint64_t)height << 16) | ((uint64_t)ncams << 32);
-        if ((s = ensure_tile_order(c, tiles_x, tiles_y, ncams, key))) return s;
+        if ((s = ensure_tile_order(c, tiles_x, tiles_y, ncams, tiles ? &c->h_tiles : nullptr))) return s;
         a.tile_bucket = c->d_tbucket;
         a.tile_hist = c->d_thist + TILE_BUCKETS * c->ord_parity;
-        if (c->ord_ready) a.tiles = c->d_order;  // every tile once, costliest first
+        if (!tiles) a.tiles = c->d_tcode;
+        if (c->ord_ready) a.perm = c->d_order;
     }
     a.ntiles = nwork;
     const uint64_t npix = out->packed ? nwork * 64 : (uint64_t)width * height * ncams;

@@ -131,7 +131,8 @@ struct RenderArgs {
     float* ray_dirs;
     uint32_t* hit_counts;
     unsigned long long* stats;  // [crossings, accepted, rounds] or null
-    uint8_t* tile_bucket;       // per tile (cam, ty, tx row-major): log-scale cost class of its wave, or null
+    const uint32_t* perm;       // dispatch order: workgroup -> tile-list position (cost-ordered), or null
+    uint8_t* tile_bucket;       // per tile-list position: log-scale cost class of its wave, or null
     uint32_t* tile_hist;        // tiles per cost class (TILE_BUCKETS), for the next frame's order
 };
 

@@ -73,14 +73,15 @@ struct gvrt_context {
     double async_ms_sum = 0.0;         // kernel times of async launches drained before the next gvrt_sync
     uint64_t async_drained = 0;
     // cost-ordered dispatch: the previous launch's per-tile cost classes, tiles ordered costliest first
-    uint64_t ord_key = 0;            // width | height << 16 | ncams << 32 of the arrays below
+    uint64_t ord_key = 0;            // width | height << 16 | ncams << 32 (| 1 << 63: full frame) of the arrays below
+    std::vector<uint32_t> ord_list;  // the caller's tile list the order belongs to (empty: full frame)
     uint64_t ord_n = 0;              // tiles
-    bool ord_ready = false;          // d_order holds an order for ord_key
-    uint8_t* d_tbucket = nullptr;    // per tile: cost class of the last launch
+    bool ord_ready = false;          // d_order holds an order for ord_key / ord_list
+    uint8_t* d_tbucket = nullptr;    // per tile-list position: cost class of the last launch
     uint32_t* d_thist = nullptr;     // [class counts, fill cursors] x launch parity (gvrt_render.hip)
     uint32_t ord_parity = 0;         // parity of the next launch
-    uint32_t* d_tcode = nullptr;     // per tile: packed tile code (cam << 24 | ty << 12 | tx)
-    uint32_t* d_order = nullptr;     // tile codes, costliest class first
+    uint32_t* d_tcode = nullptr;     // full frames: the tile list (cam << 24 | ty << 12 | tx), supertile order
+    uint32_t* d_order = nullptr;     // dispatch order: tile-list positions, costliest class first
     void* d_stage = nullptr;  // staging for host outputs
     uint64_t stage_cap = 0;
 

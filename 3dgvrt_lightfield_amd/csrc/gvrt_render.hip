@@ -500,7 +500,8 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
     const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     // (Round-robin workgroup -> XCD dealing is kept: an XCD-contiguous band remap measured 33 % slower,
     // the bands' very different costs leave a long tail; L2 hit rate is already ~91 %.)
-    const uint64_t tile_idx = (uint64_t)blockIdx.x * WGW + wid;  // tile-list position
+    // tile-list position: the cost-ordered permutation of the list, or the workgroup's own
+    const uint64_t tile_idx = a.perm ? (uint64_t)a.perm[blockIdx.x] : (uint64_t)blockIdx.x * WGW + wid;
     uint32_t cam, tx, ty;
     if (tiles_) {
         if (tile_idx >= a.ntiles) return;  // wave-uniform
@@ -972,7 +973,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
     const uint32_t pxy = s_pxy[wid][olane];
     const uint32_t opx = pxy & 0xFFFFu, opy = pxy >> 16;
     const bool ovalid = opx < a.width && opy < a.height && cam < a.ncams;
-    const uint64_t otile = (uint64_t)blockIdx.x * WGW + (uint32_t)wid;
+    const uint64_t otile = a.perm ? (uint64_t)a.perm[blockIdx.x] : (uint64_t)blockIdx.x * WGW + (uint32_t)wid;
     if (ovalid) {
         const uint64_t pix = ((uint64_t)cam * a.height + opy) * a.width + opx;
         const uint64_t oi = a.packed ? otile * 64 + olane : pix;
@@ -999,13 +1000,12 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
         if (hit_counts_) hit_counts_[oi] = 0u;
     }
     if (a.tile_bucket && olane == 0) {
-        // this tile's cost class, 4 per octave of its cycles (vector stores / atomics from lane 0); tile
-        // coordinates from lane 0's pixel
+        // this tile's cost class, 4 per octave of its cycles, at its tile-list position (vector store and
+        // atomic from lane 0)
         const uint64_t cyc = __builtin_amdgcn_s_memtime() - s_t0[wid];
         const float lc = 4.0f * __log2f((float)cyc + 1.0f) - 40.0f;  // 1 k cycles: class 0
         const uint32_t b = (uint32_t)fminf(fmaxf(lc, 0.0f), (float)(TILE_BUCKETS - 1));
-        const uint32_t tid = (cam * a.tiles_y + (opy >> 3)) * a.tiles_x + (opx >> 3);
-        a.tile_bucket[tid] = (uint8_t)b;
+        a.tile_bucket[otile] = (uint8_t)b;
         atomicAdd(a.tile_hist + b, 1u);
     }
     if constexpr (STATS) {
@@ -1115,14 +1115,15 @@ extern "C" int gvrt_debug_trace_get(float* out, int maxn) {
 }
 #endif
 
-// The next launch's tile order from this launch's cost classes, costliest class first.  Class counts and
+// The next launch's dispatch order (a permutation of tile-list positions) from this launch's cost classes,
+// costliest class first.  Class counts and
 // fill cursors are double-buffered by launch parity: the render kernel of launch k counts into hist[k & 1],
 // this kernel turns them into class starts (every block computes the 64-entry prefix), places each tile at
 // start + cursor (ranks within a block by LDS atomics, one global atomic per class per block) and clears the
 // other parity's arrays for launch k + 1.  Order within a class is arbitrary (it
 // changes only which wave renders a tile when).
 __global__ __launch_bounds__(256) void k_tile_order(uint32_t n, const uint8_t* __restrict__ bucket,
-                                                    const uint32_t* __restrict__ code, uint32_t* __restrict__ hist,
+                                                    uint32_t* __restrict__ hist,
                                                     uint32_t* __restrict__ fill, uint32_t* __restrict__ hist_next,
                                                     uint32_t* __restrict__ fill_next, uint32_t* __restrict__ order) {
     __shared__ uint32_t base[TILE_BUCKETS];
@@ -1146,7 +1147,7 @@ __global__ __launch_bounds__(256) void k_tile_order(uint32_t n, const uint8_t* _
     __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (total != n) {  // counts not from one complete launch (never expected): the plain order, every tile once
-        if (i < n) order[i] = code[i];
+        if (i < n) order[i] = i;
         return;
     }
     const uint32_t b = i < n ? bucket[i] : 0u;
@@ -1156,7 +1157,7 @@ __global__ __launch_bounds__(256) void k_tile_order(uint32_t n, const uint8_t* _
     __syncthreads();
     if (i < n) {
         const uint32_t pos = base[b] + off[b] + r;
-        if (pos < n) order[pos] = code[i];
+        if (pos < n) order[pos] = i;
     }
 }
 
@@ -1164,7 +1165,7 @@ gvrt_status gvrt_launch_tile_order(gvrt_context* c) {
     const uint32_t p = c->ord_parity;
     uint32_t* h = c->d_thist;  // [hist 0, hist 1, fill 0, fill 1] x TILE_BUCKETS
     const uint32_t n = (uint32_t)c->ord_n;
-    hipLaunchKernelGGL(k_tile_order, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, c->d_tbucket, c->d_tcode,
+    hipLaunchKernelGGL(k_tile_order, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, c->d_tbucket,
                        h + TILE_BUCKETS * p, h + TILE_BUCKETS * (2 + p), h + TILE_BUCKETS * (1 - p),
                        h + TILE_BUCKETS * (3 - p), c->d_order);
     GVRT_HIP(c, hipGetLastError());
