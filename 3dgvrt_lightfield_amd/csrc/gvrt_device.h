@@ -24,7 +24,11 @@ constexpr float IPHI = 0.618033988749895f;
 constexpr float ICOSA_VRT_SCALE = 0.5f * 1.323169076499215f;  // particlePrimitives.comp:78-79
 constexpr float SQRT3 = 1.7320508075688772f;
 constexpr int STACK_DEPTH = 128;                      // per-wave LDS traversal stack
-constexpr int TILE_BUCKETS = 64;                      // cost classes of the cost-ordered dispatch (4 per octave)
+#ifndef GVRT_TILE_CPO
+#define GVRT_TILE_CPO 4  // cost classes per octave of the cost-ordered dispatch
+#endif
+constexpr int TILE_CPO = GVRT_TILE_CPO;
+constexpr int TILE_BUCKETS = 16 * TILE_CPO;           // classes: 1 k .. 64 M cycles
 
 struct alignas(16) RenderRec {
     float px, py, pz, density;

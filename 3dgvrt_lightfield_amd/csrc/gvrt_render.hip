@@ -1003,7 +1003,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
         // this tile's cost class, 4 per octave of its cycles, at its tile-list position (vector store and
         // atomic from lane 0)
         const uint64_t cyc = __builtin_amdgcn_s_memtime() - s_t0[wid];
-        const float lc = 4.0f * __log2f((float)cyc + 1.0f) - 40.0f;  // 1 k cycles: class 0
+        const float lc = (float)TILE_CPO * (__log2f((float)cyc + 1.0f) - 10.0f);  // 1 k cycles: class 0
         const uint32_t b = (uint32_t)fminf(fmaxf(lc, 0.0f), (float)(TILE_BUCKETS - 1));
         a.tile_bucket[otile] = (uint8_t)b;
         atomicAdd(a.tile_hist + b, 1u);

@@ -106,3 +106,14 @@ def test_bicycle_device_quality_build(gv, O):
     finally:
         sc.close()
     _cmp_images(a["rgba32f"].reshape(-1, 4)[sub.astype(np.int64)], ref)
+
+
+@pytest.mark.parametrize("cfg", ["garden", "truck"])
+def test_device_sah_equals_host_large(gv, cfg):
+    """The 3 M (garden) and 2 M (truck) stand-ins: device and host quality builds give the same trees."""
+    gen, _, _, _ = gv.scene.CONFIGS[cfg]
+    with gv.Renderer(0) as r:
+        r.prepare(gv.scene.make(**gen))
+        out = _build_pair(r)
+        _check_pair(out)
+        print(f"{cfg}: device {out[2, 1][3]:.1f} ms, host {out[3, 1][3]:.1f} ms, {out[2, 1][2]} nodes")
