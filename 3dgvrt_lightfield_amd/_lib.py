@@ -111,6 +111,7 @@ SIGNATURES = {
     "gvrt_render_async": (C.c_int32, [H, _P(RenderParams), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
                                 C.c_uint32, C.c_void_p, C.c_uint64, _P(Image)]),
     "gvrt_sync": (C.c_int32, [H]),
+    "gvrt_set_stream": (C.c_int32, [H, C.c_void_p]),
     "gvrt_set_stats": (C.c_int32, [H, C.c_int]),
     "gvrt_get_device_properties": (C.c_int32, [C.c_int, _P(DeviceProperties)]),
     "gvrt_get_device_buffers": (C.c_int32, [H, _P(DeviceBuffers)]),

@@ -114,7 +114,8 @@ gvrt_status gvrt_create(int device, gvrt_handle* out) {
     if (!c) return gvrt_fail(nullptr, GVRT_ERR_OOM, "host allocation failed");
     c->device = device;
     e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    c->stream = c->own_stream;
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
     if (e != hipSuccess) {
@@ -141,7 +142,7 @@ gvrt_status gvrt_destroy(gvrt_handle c) {
     for (hipEvent_t e : c->async_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return GVRT_OK;
 }
@@ -360,6 +361,30 @@ static gvrt_status finish_async(gvrt_context* c) {
 // a queue deeper than this many launches waits for the queued ones first (bounds the event pool)
 constexpr uint32_t MAX_ASYNC_PENDING = 1024;
 
+// Encode a caller tile list (cam << 24 | ty << 12 | tx) and upload it only when it differs from what the
+// device buffer already holds: a static split (the multi-GPU tile list) then costs no host round trip per
+// frame, so frames queue back to back.  A changed list waits for queued launches first (they may read the
+// buffer, and the host copy is the source of the pageable upload).
+static gvrt_status upload_tile_list(gvrt_context* c, const gvrt_tile* tiles, uint64_t ntiles, uint32_t tiles_x,
+                                    uint32_t tiles_y, uint32_t ncams, std::vector<uint32_t>& host, uint32_t** dev,
+                                    uint64_t* cap, bool& valid) {
+    std::vector<uint32_t> tl(ntiles);
+    for (uint64_t i = 0; i < ntiles; ++i) {
+        if (tiles[i].tx >= tiles_x || tiles[i].ty >= tiles_y || tiles[i].cam >= ncams)
+            return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "tile outside the image");
+        tl[i] = ((uint32_t)tiles[i].cam << 24) | ((uint32_t)tiles[i].ty << 12) | tiles[i].tx;
+    }
+    if (valid && tl == host) return GVRT_OK;
+    if (c->async_pending) GVRT_HIP(c, hipStreamSynchronize(c->stream));
+    valid = false;
+    host.swap(tl);
+    gvrt_status s;
+    if ((s = ensure(c, (void**)dev, cap, 4 * (ntiles ? ntiles : 1)))) return s;
+    if (ntiles) GVRT_HIP(c, hipMemcpyAsync(*dev, host.data(), 4 * ntiles, hipMemcpyHostToDevice, c->stream));
+    valid = true;
+    return GVRT_OK;
+}
+
 // Cost-ordered dispatch.  A tile's render time varies ~4x across the frame (scene depth complexity), and
 // with the default row-major supertile order the costly tiles that start last set a tail of ~27 % over a
 // perfectly balanced schedule (list-scheduling model on measured per-tile cycles).  Each
@@ -503,16 +528,9 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "kbuffer_depth must be 0, 8, 12, 16, 20, 24 or 32");
     uint64_t nwork = total_tiles;
     if (tiles) {
-        if (c->async_pending) GVRT_HIP(c, hipStreamSynchronize(c->stream));  // h_tiles may feed a pending upload
-        std::vector<uint32_t>& tl = c->h_tiles;
-        tl.resize(ntiles);
-        for (uint64_t i = 0; i < ntiles; ++i) {
-            if (tiles[i].tx >= tiles_x || tiles[i].ty >= tiles_y || tiles[i].cam >= ncams)
-                return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "tile outside the image");
-            tl[i] = ((uint32_t)tiles[i].cam << 24) | ((uint32_t)tiles[i].ty << 12) | tiles[i].tx;
-        }
-        if ((s = ensure(c, (void**)&c->d_tiles, &c->tiles_cap, 4 * (ntiles ? ntiles : 1)))) return s;
-        if (ntiles) GVRT_HIP(c, hipMemcpyAsync(c->d_tiles, tl.data(), 4 * ntiles, hipMemcpyHostToDevice, c->stream));
+        if ((s = upload_tile_list(c, tiles, ntiles, tiles_x, tiles_y, ncams, c->h_tiles, &c->d_tiles, &c->tiles_cap,
+                                  c->tiles_valid)))
+            return s;
         a.tiles = c->d_tiles;
         nwork = ntiles;
     }
@@ -625,24 +643,53 @@ gvrt_status gvrt_sync(gvrt_handle c) {
     return finish_async(c);
 }
 
+gvrt_status gvrt_set_stream(gvrt_handle c, void* stream) {
+    if (!c) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL handle");
+    GVRT_HIP(c, hipSetDevice(c->device));
+    gvrt_status s;
+    if (c->async_pending && (s = drain_async(c))) return s;  // their kernel times stay counted for gvrt_sync
+    GVRT_HIP(c, hipStreamSynchronize(c->stream));
+    c->stream = stream ? reinterpret_cast<hipStream_t>(stream) : c->own_stream;
+    return GVRT_OK;
+}
+
 gvrt_status gvrt_unpack_tiles_rgba8(gvrt_handle c, const void* packed, const gvrt_tile* tiles, uint64_t ntiles,
                                     uint32_t width, uint32_t height, uint32_t ncams, void* frame) {
     if (!c || !packed || !tiles || !frame) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL argument");
     if (width == 0 || height == 0 || width > 32768 || height > 32768 || ncams == 0 || ncams > 255)
         return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "frame must be 1..32768 pixels per side, 1..255 cameras");
     const uint32_t tiles_x = (width + 7) / 8, tiles_y = (height + 7) / 8;
-    std::vector<uint32_t> tl(ntiles);
-    for (uint64_t i = 0; i < ntiles; ++i) {  // the packed tile word carries tx, ty in 12 bits and cam in 8
-        if (tiles[i].tx >= tiles_x || tiles[i].ty >= tiles_y || tiles[i].cam >= ncams)
-            return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "tile outside the frame");
-        tl[i] = ((uint32_t)tiles[i].cam << 24) | ((uint32_t)tiles[i].ty << 12) | tiles[i].tx;
-    }
     GVRT_HIP(c, hipSetDevice(c->device));
     gvrt_status s;
-    if (c->async_pending && (s = finish_async(c))) return s;  // queued renders may still read d_tiles
-    if ((s = ensure(c, (void**)&c->d_tiles, &c->tiles_cap, 4 * (ntiles ? ntiles : 1)))) return s;
-    if (ntiles) GVRT_HIP(c, hipMemcpyAsync(c->d_tiles, tl.data(), 4 * ntiles, hipMemcpyHostToDevice, c->stream));
-    if ((s = gvrt_launch_unpack(c, packed, c->d_tiles, ntiles, width, height, frame))) return s;
+    // the cached list equal to this one, else the least recently used of up to UNPACK_LISTS buffers
+    constexpr size_t UNPACK_LISTS = 16;
+    auto& L = c->unpack_lists;
+    size_t pick = L.size();
+    for (size_t i = 0; i < L.size(); ++i)
+        if (L[i].valid && L[i].host.size() == ntiles) {
+            bool same = true;
+            for (uint64_t j = 0; j < ntiles && same; ++j)
+                same = L[i].host[j] == (((uint32_t)tiles[j].cam << 24) | ((uint32_t)tiles[j].ty << 12) | tiles[j].tx);
+            if (same) {
+                pick = i;
+                break;
+            }
+        }
+    if (pick == L.size()) {
+        if (L.size() < UNPACK_LISTS) {
+            L.emplace_back();
+        } else {
+            pick = 0;
+            for (size_t i = 1; i < L.size(); ++i)
+                if (L[i].used < L[pick].used) pick = i;
+        }
+    }
+    gvrt_context::TileListBuf& b = L[pick];
+    b.used = ++c->unpack_calls;
+    if ((s = upload_tile_list(c, tiles, ntiles, tiles_x, tiles_y, ncams, b.host, &b.dev, &b.cap, b.valid))) return s;
+    if ((s = gvrt_launch_unpack(c, packed, b.dev, ntiles, width, height, frame))) return s;
+    // behind queued renders (gvrt_render_async) the unpack is queued too and completes by gvrt_sync
+    if (c->async_pending) return GVRT_OK;
     GVRT_HIP(c, hipStreamSynchronize(c->stream));
     return GVRT_OK;
 }

@@ -12,6 +12,7 @@
 struct gvrt_context {
     int device = -1;
     hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;  // created with the handle; stream is it unless gvrt_set_stream chose another
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::string err;
     uint64_t device_bytes = 0;
@@ -67,7 +68,19 @@ struct gvrt_context {
     float* d_viewinv = nullptr;
     uint64_t viewinv_cap = 0;
     std::vector<float> h_viewinv;  // host copy of what d_viewinv holds
-    std::vector<uint32_t> h_tiles; // host copy of the last tile list (source of an async upload)
+    std::vector<uint32_t> h_tiles; // host copy of what d_tiles holds (uploaded only when the list changes)
+    bool tiles_valid = false;      // d_tiles holds h_tiles
+    // gvrt_unpack_tiles_rgba8's lists (own buffers: queued renders may read d_tiles): one per rank part of a
+    // split frame, so that assembling a static split uploads nothing per frame
+    struct TileListBuf {
+        std::vector<uint32_t> host;
+        uint32_t* dev = nullptr;
+        uint64_t cap = 0;
+        bool valid = false;
+        uint64_t used = 0;  // last use (LRU)
+    };
+    std::vector<TileListBuf> unpack_lists;
+    uint64_t unpack_calls = 0;
     std::vector<hipEvent_t> async_ev;  // event pairs of queued gvrt_render_async launches
     uint32_t async_pending = 0;
     double async_ms_sum = 0.0;         // kernel times of async launches drained before the next gvrt_sync

@@ -209,6 +209,11 @@ class Renderer:
         """gvrt_sync: wait for the frames queued by render_device(async_=True); render_ms() is then their mean."""
         check(lib().gvrt_sync(self.h), self.h)
 
+    def set_stream(self, stream_ptr):
+        """gvrt_set_stream: launch on this hipStream_t (an integer, e.g. torch.cuda.current_stream().cuda_stream;
+        0 / None: the handle's own stream)."""
+        check(lib().gvrt_set_stream(self.h, C.c_void_p(stream_ptr or None)), self.h)
+
     def unpack_tiles_rgba8(self, packed_ptr, tiles, width, height, frame_ptr, ncams=1):
         """gvrt_unpack_tiles_rgba8: tile-packed rgba8 (device) -> frame [ncams][H][W][4] (device)."""
         t, nt = self.tile_array(tiles)

@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true", help="skip the LITERAL stats pass (roofline bytes)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes (roofline.traffic, VALU)")
+    ap.add_argument("--exchange", action="store_true",
+                    help="run the multi-GPU frame-exchange path even with one rank (torch.distributed.run "
+                         "--nproc-per-node 1: rehearses the N-rank step on one GPU)")
     ap.add_argument("--build", default="quality", choices=["quality", "fast"],
                     help="quality: device binned-SAH tree + SAH-optimal 4-wide collapse (the static-scene build, "
                          "as the reference's PREFER_FAST_TRACE BLAS); fast: device LBVH + greedy collapse")
@@ -154,7 +157,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    distributed = world > 1
+    distributed = world > 1 or (args.exchange and "RANK" in os.environ)
     pmc = None
     if not distributed and not args.no_pmc:
         pmc = pmc_passes(args)  # before this process touches the GPU
@@ -232,18 +235,24 @@ def main():
                 for p, t in zip(parts, all_tiles):
                     r.unpack_tiles_rgba8(p.data_ptr(), t, W, H, full.data_ptr())
 
+        # Frames are queued as on one GPU (gvrt_render_async), on torch's stream (gvrt_set_stream): the
+        # gather of a frame is posted behind its render, the wait for the gather that last used a buffer
+        # (work.wait) precedes the next render into it, all ordered on the device with no host round trip.
+        r.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         ex = dist_mod.FrameExchange(dist, rank, world, part_sizes, item_shape, torch.uint8, dev, nbuf=2,
-                                    assemble=assemble, sync=lambda: torch.cuda.current_stream().synchronize())
+                                    assemble=assemble, sync=None)
 
-        def render_into(buf):  # synchronous render on the library's stream, straight into the send buffer
-            r.render_device(vi, pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=buf.data_ptr(), packed=packed)
-            kernel_ms.append(r.render_ms())
+        def render_into(buf):
+            r.render_device(vi, pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=buf.data_ptr(), packed=packed,
+                            async_=True)
 
         def step():
             ex.step(render_into)
 
         def drain():
             ex.drain()
+            r.sync()
+            kernel_ms.append(r.render_ms())  # mean over the queued launches
     else:
         # One GPU: frames are queued back to back (gvrt_render_async; one host round trip per K frames instead
         # of one per frame); the kernel time is the mean over the queued launches (HIP event pairs), at sync.

@@ -204,6 +204,14 @@ gvrt_status gvrt_render_async(gvrt_handle h, const gvrt_render_params* p, const 
                               const gvrt_image* out);
 gvrt_status gvrt_sync(gvrt_handle h);
 
+/* Launch on the caller's HIP stream (a hipStream_t; NULL: the handle's own stream again), as a BLAS
+ * handle's set-stream does: the caller's work on that stream is then ordered with the renders without a
+ * host round trip or a cross-stream event.  The multi-GPU frame exchange renders on the stream its
+ * gathers are posted from (the reference chains its per-frame submits with semaphores,
+ * VulkanRTBase.cpp:983-1059).  Waits for the work queued on the previous stream first; the stream must
+ * outlive its use by the handle. */
+gvrt_status gvrt_set_stream(gvrt_handle h, void* stream);
+
 /* Device identity for the benchmark report: the VkPhysicalDeviceProperties fields vks::Benchmark
  * prints and writes to fps.txt (deviceName, driverVersion; base/benchmark.hpp:23,67-70,85). */
 typedef struct {
@@ -242,7 +250,8 @@ gvrt_status gvrt_get_stats(gvrt_handle h, gvrt_stats* s);
 
 /* Scatter a tile-packed rgba8 buffer (gathered from ranks) into a full frame [ncams][H][W][4]; device
  * ptrs.  Every tile must lie inside the frame (tx < ceil(W/8), ty < ceil(H/8), cam < ncams), else
- * GVRT_ERR_INVALID_ARG and nothing is written. */
+ * GVRT_ERR_INVALID_ARG and nothing is written.  Runs on the handle's stream behind any queued
+ * gvrt_render_async launches: synchronous when none are queued, else it completes by gvrt_sync. */
 gvrt_status gvrt_unpack_tiles_rgba8(gvrt_handle h, const void* packed, const gvrt_tile* tiles,
                                     uint64_t ntiles, uint32_t width, uint32_t height, uint32_t ncams,
                                     void* frame);

@@ -4,6 +4,8 @@ Error behaviour follows the reference's VK_CHECK_RESULT policy moved to the call
 returns a status (GvrtError here) and leaves the handle usable.  Limits: 32768 pixels per side, 255
 cameras per launch (tile words carry the camera in 8 bits).
 """
+import importlib
+
 import numpy as np
 import pytest
 
@@ -180,3 +182,34 @@ def test_cost_ordered_dispatch_changes_no_pixel(gv, config1):
         for tx, ty, _, _ in t:
             np.testing.assert_array_equal(part[8 * ty:8 * ty + 8, 8 * tx:8 * tx + 8],
                                           first["rgba32f"][0][8 * ty:8 * ty + 8, 8 * tx:8 * tx + 8])
+
+
+def test_caller_stream_queued_split_frame(gv, config1):
+    """The multi-GPU exchange's device-side pipeline on one GPU: renders queued (gvrt_render_async) on a
+    caller stream (gvrt_set_stream), each rank part of a tile-split frame rendered tile-packed, then all parts
+    unpacked behind the queued renders (gvrt_unpack_tiles_rgba8 with renders pending: queued, done by
+    gvrt_sync), repeated with the same static tile lists (uploaded once, no host round trip) — the frame
+    equals the synchronous full-frame render; back on the handle's own stream nothing changes."""
+    import torch
+    W, H = 200, 120
+    vi, pi = gv.scene.config1_camera(W, H)
+    world = 3
+    parts = importlib.import_module("3dgvrt_lightfield_amd.dist").rank_tiles(W, H, 1, world, block=2)
+    with gv.Renderer(0) as r:
+        r.prepare(config1)
+        ref = r.render(vi, pi, W, H)["rgba8"][0]
+        s = torch.cuda.Stream()
+        r.set_stream(s.cuda_stream)
+        bufs = [torch.zeros((t.shape[0] * 64, 4), dtype=torch.uint8, device="cuda") for t in parts]
+        frames = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(2)]
+        for it in range(4):
+            frame = frames[it % 2]
+            for b, t in zip(bufs, parts):
+                r.render_device(vi, pi, W, H, tiles=t, rgba8_ptr=b.data_ptr(), packed=True, async_=True)
+            for b, t in zip(bufs, parts):
+                r.unpack_tiles_rgba8(b.data_ptr(), t, W, H, frame.data_ptr())
+        r.sync()
+        for frame in frames:
+            np.testing.assert_array_equal(frame.cpu().numpy(), ref)
+        r.set_stream(None)
+        np.testing.assert_array_equal(r.render(vi, pi, W, H)["rgba8"][0], ref)
