@@ -210,8 +210,9 @@ class Renderer:
         check(lib().gvrt_sync(self.h), self.h)
 
     def set_stream(self, stream_ptr):
-        """gvrt_set_stream: launch on this hipStream_t (an integer, e.g. torch.cuda.current_stream().cuda_stream;
-        0 / None: the handle's own stream)."""
+        """gvrt_set_stream: launch on this hipStream_t (an integer, e.g. torch.cuda.Stream().cuda_stream;
+        0 / None: the handle's own stream — torch's default stream is the NULL stream, which the handle's
+        non-blocking stream does not order with, so share a non-default torch stream)."""
         check(lib().gvrt_set_stream(self.h, C.c_void_p(stream_ptr or None)), self.h)
 
     def unpack_tiles_rgba8(self, packed_ptr, tiles, width, height, frame_ptr, ncams=1):

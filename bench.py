@@ -238,7 +238,10 @@ def main():
         # Frames are queued as on one GPU (gvrt_render_async), on torch's stream (gvrt_set_stream): the
         # gather of a frame is posted behind its render, the wait for the gather that last used a buffer
         # (work.wait) precedes the next render into it, all ordered on the device with no host round trip.
-        r.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        xs = torch.cuda.Stream(dev)  # not the null stream: the handle's own stream does not order with it
+        torch.cuda.synchronize()
+        torch.cuda.set_stream(xs)
+        r.set_stream(xs.cuda_stream)
         ex = dist_mod.FrameExchange(dist, rank, world, part_sizes, item_shape, torch.uint8, dev, nbuf=2,
                                     assemble=assemble, sync=None)
 

@@ -209,7 +209,8 @@ gvrt_status gvrt_sync(gvrt_handle h);
  * host round trip or a cross-stream event.  The multi-GPU frame exchange renders on the stream its
  * gathers are posted from (the reference chains its per-frame submits with semaphores,
  * VulkanRTBase.cpp:983-1059).  Waits for the work queued on the previous stream first; the stream must
- * outlive its use by the handle. */
+ * outlive its use by the handle.  The handle's own stream is non-blocking: work on the legacy NULL
+ * stream is not ordered with it, so a caller that posts its work there cannot share it this way. */
 gvrt_status gvrt_set_stream(gvrt_handle h, void* stream);
 
 /* Device identity for the benchmark report: the VkPhysicalDeviceProperties fields vks::Benchmark
