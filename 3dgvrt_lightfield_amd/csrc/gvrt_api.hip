@@ -523,6 +523,16 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
     a.max_rounds = p->max_rounds;
     a.ray_dirs_layout = p->ray_dirs_layout;
     a.packed = out->packed;
+    // no per-child box slack when the absolute box padding covers the plane rounding for every camera of
+    // the launch (|origin component| <= 4 x the scene's position bound; split pieces keep the slack)
+    {
+        float omax = 0.0f;
+        for (uint32_t i = 0; i < ncams; ++i)
+            for (int k = 12; k < 15; ++k) omax = std::max(omax, std::fabs(view_inverse[16ull * i + k]));
+        static const bool slack_forced = getenv("GVRT_BOX_SLACK") && getenv("GVRT_BOX_SLACK")[0] == '1';
+        a.box_exact = !slack_forced && !c->split_cells && c->box_pad_abs > 0.0f &&
+                      std::ldexp(omax, -20) <= c->box_pad_abs;  // also false for a NaN origin
+    }
     a.kfast = p->kbuffer_depth ? p->kbuffer_depth : (uint32_t)K_FAST_DEFAULT;
     if (a.kfast != 8 && a.kfast != 12 && a.kfast != 16 && a.kfast != 20 && a.kfast != 24 && a.kfast != 32)
         return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "kbuffer_depth must be 0, 8, 12, 16, 20, 24 or 32");

@@ -110,7 +110,22 @@ struct EncloseArgs {
     uint32_t* src;
     RenderRec* recs;
     float* boxes;
+    const uint32_t* absmax;  // bits of the largest finite |position component| (k_pos_absmax)
 };
+
+// Largest finite |position component| of the splats (float bits: non-negative floats order as their bits).
+// The proxy boxes get an absolute padding of 2^-18 x this bound: it covers the rounding of the render
+// kernel's FMA-form box planes for ray origins within 4x the bound, so that kernel needs no per-box slack.
+__global__ __launch_bounds__(256) void k_pos_absmax(uint64_t n3, const float* __restrict__ pos,
+                                                    uint32_t* __restrict__ out) {
+    float m = 0.0f;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n3; i += (uint64_t)gridDim.x * blockDim.x) {
+        const float v = fabsf(pos[i]);
+        if (v <= 3.0e38f) m = fmaxf(m, v);  // NaN / inf positions do not set the bound
+    }
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
 
 // particlePrimitives.comp:142-214
 __global__ __launch_bounds__(256) void k_enclose_emit(EncloseArgs a) {
@@ -165,10 +180,11 @@ __global__ __launch_bounds__(256) void k_enclose_emit(EncloseArgs a) {
     // Proxy AABB, padded so the analytic icosahedron of the render kernel (exact planes) is
     // always inside the box built from the rounded vertices.
     float* bx = a.boxes + 6ull * saveIdx;
+    const float pad_abs = ldexpf(__uint_as_float(*a.absmax), -18);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const float c = 0.5f * (lo[k] + hi[k]);
-        const float pad = 1e-5f * (hi[k] - lo[k]) + 1e-6f * fabsf(c) + 1e-30f;
+        const float pad = 1e-5f * (hi[k] - lo[k]) + 1e-6f * fabsf(c) + pad_abs + 1e-30f;
         bx[k] = lo[k] - pad;
         bx[3 + k] = hi[k] + pad;
     }
@@ -227,6 +243,10 @@ gvrt_status gvrt_launch_enclose(gvrt_context* c, const gvrt_enclosing_params* p,
         if ((s = gvrt_dalloc(c, (void**)&c->d_scan, 4 * (nn + 1)))) return s;
         c->cap = nn;
     }
+    if (!c->d_absmax) {
+        gvrt_status s;
+        if ((s = gvrt_dalloc(c, (void**)&c->d_absmax, 4))) return s;
+    }
     gvrt_dfree(c, (void**)&c->d_verts);
     gvrt_dfree(c, (void**)&c->d_tris);
     if (p->emit_triangles && n) {
@@ -236,6 +256,7 @@ gvrt_status gvrt_launch_enclose(gvrt_context* c, const gvrt_enclosing_params* p,
     }
     if (n == 0) {
         *m_out = 0;
+        c->box_pad_abs = 0.0f;
         return GVRT_OK;
     }
     const unsigned blocks = (unsigned)((n + 255) / 256);
@@ -254,6 +275,19 @@ gvrt_status gvrt_launch_enclose(gvrt_context* c, const gvrt_enclosing_params* p,
     if (e != hipSuccess) {
         gvrt_dfree(c, &tmp);
         return gvrt_hip_check(c, e, "DeviceScan::ExclusiveSum");
+    }
+    // scene position bound for the absolute box padding (read by k_enclose_emit on the device)
+    uint32_t* d_absmax = c->d_absmax;
+    GVRT_HIP(c, hipMemsetAsync(d_absmax, 0, 4, c->stream));
+    {
+        const uint64_t n3 = 3 * n;
+        const unsigned rb = (unsigned)std::min<uint64_t>((n3 + 255) / 256, 2048);
+        hipLaunchKernelGGL(k_pos_absmax, dim3(rb), dim3(256), 0, c->stream, n3, c->d_pos, d_absmax);
+        e = hipGetLastError();
+        if (e != hipSuccess) {
+            gvrt_dfree(c, &tmp);
+            return gvrt_hip_check(c, e, "k_pos_absmax");
+        }
     }
     EncloseArgs a;
     a.n = n;
@@ -275,6 +309,7 @@ gvrt_status gvrt_launch_enclose(gvrt_context* c, const gvrt_enclosing_params* p,
     a.src = c->d_src;
     a.recs = c->d_recs_c;
     a.boxes = c->d_boxes_c;
+    a.absmax = d_absmax;
     hipLaunchKernelGGL(k_enclose_emit, dim3(blocks), dim3(256), 0, c->stream, a);
     e = hipGetLastError();
     if (e != hipSuccess) {
@@ -292,9 +327,13 @@ gvrt_status gvrt_launch_enclose(gvrt_context* c, const gvrt_enclosing_params* p,
         }
     }
     GVRT_HIP(c, hipEventRecord(c->ev1, c->stream));
-    uint32_t count = 0;
+    uint32_t count = 0, absmax = 0;
     GVRT_HIP(c, hipMemcpyAsync(&count, c->d_scan + n, 4, hipMemcpyDeviceToHost, c->stream));
+    GVRT_HIP(c, hipMemcpyAsync(&absmax, d_absmax, 4, hipMemcpyDeviceToHost, c->stream));
     GVRT_HIP(c, hipStreamSynchronize(c->stream));
+    float r;
+    std::memcpy(&r, &absmax, 4);
+    c->box_pad_abs = std::ldexp(r, -18);
     gvrt_dfree(c, &tmp);
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);

@@ -39,6 +39,8 @@ struct gvrt_context {
     uint32_t* d_src = nullptr;
     gvrt::RenderRec* d_recs_c = nullptr;
     float* d_boxes_c = nullptr;  // 6 per survivor
+    uint32_t* d_absmax = nullptr;  // k_pos_absmax result (float bits)
+    float box_pad_abs = 0.0f;      // absolute proxy-box padding of the last enclose: 2^-18 x max |position|
     uint32_t* d_flags = nullptr;
     uint32_t* d_scan = nullptr;
 

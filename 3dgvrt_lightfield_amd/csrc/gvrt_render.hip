@@ -98,6 +98,7 @@ __device__ unsigned long long g_trace_pix;
 // Slab test, optionally in FMA form t = lo * inv - o * inv (one v_fma per plane).  Culling only: the proxy boxes
 // are padded (1e-5 extent + 1e-6 |centre|, gvrt_enclose.hip) and a relative slack on the exit
 // distance absorbs the rounding, so a crossing is never dropped.
+template <bool SLACK>
 __device__ inline bool box_hit(float lx, float ly, float lz, float hx, float hy, float hz, f3 o, f3 oinv, f3 inv,
                                float t0, float t1, float& tenter) {
 #if GVRT_FMA_BOX
@@ -114,7 +115,12 @@ __device__ inline bool box_hit(float lx, float ly, float lz, float hx, float hy,
     const float tn = fmaxf(fmaxf(t0, fminf(ax, bx)), fmaxf(fminf(ay, by), fminf(az, bz)));
     const float tf = fminf(fminf(t1, fmaxf(ax, bx)), fminf(fmaxf(ay, by), fmaxf(az, bz)));
     tenter = tn;
-    return tn <= tf + 2e-6f * fabsf(tf);
+    // SLACK: a relative slack on the exit distance absorbs the plane rounding.  Without it the
+    // absolute box padding of gvrt_enclose.hip (2^-18 x the scene's position bound) covers the rounding
+    // of these FMA-form planes, (2|lo| + 3|o|) * 2^-24 per plane in world units, as long as the ray
+    // origin lies within 4x that bound (render_impl chooses the variant per launch).
+    if constexpr (SLACK) return tn <= tf + 2e-6f * fabsf(tf);
+    else return tn <= tf;
 }
 
 // Slab test on precomputed plane distances (compressed nodes)
@@ -207,6 +213,46 @@ __device__ inline uint32_t alpha_code(float alpha) {
 #ifndef GVRT_INSERT_GROUP
 #define GVRT_INSERT_GROUP 8  // 8-slot groups: fewer joins, fewer register copies (4: +4 %, 24: +2 %)
 #endif
+// GVRT_ASM_INSERT: each 8-slot group is one asm block whose slot registers are updated in place ("+v").
+// Left to the compiler, the updated slots of a group landed in fresh registers and the join with the
+// group-skip path copied the whole buffer back (~40 v_mov per executed group for 80 useful VALU).
+// Per slot: 2 v_cmp (to SGPR pairs) + 8 v_cndmask, ordered so that every mask is read at least two
+// instructions after the v_cmp that writes it (the gfx950 VALU-SGPR-write -> lane-mask-read hazard).
+#ifndef GVRT_ASM_INSERT
+#define GVRT_ASM_INSERT 1
+#endif
+#define KB_S_HEAD(T, P)                                      \
+    "v_cndmask_b32_e64 %[xt], %[pt0], " T ", %[m0]\n\t"      \
+    "v_cmp_lt_f32_e64 %[m1], %[pt1], %[xt]\n\t"              \
+    "v_cndmask_b32_e64 %[xp], %[pp0], " P ", %[m0]\n\t"      \
+    "v_cndmask_b32_e64 " T ", " T ", %[pt0], %[m0]\n\t"      \
+    "v_cndmask_b32_e64 " P ", " P ", %[pp0], %[m0]\n\t"      \
+    "v_cndmask_b32_e64 %[pt0], %[xt], %[pt1], %[m1]\n\t"
+#define KB_S_TAIL                                             \
+    "v_cndmask_b32_e64 %[pp0], %[xp], %[pp1], %[m1]\n\t"     \
+    "v_cndmask_b32_e64 %[pt1], %[pt1], %[xt], %[m1]\n\t"     \
+    "v_cndmask_b32_e64 %[pp1], %[pp1], %[xp], %[m1]\n\t"
+#define KB_S(T, P, TN) KB_S_HEAD(T, P) "v_cmp_lt_f32_e64 %[m0], %[pt0], " TN "\n\t" KB_S_TAIL
+#define KB_S_LAST(T, P) KB_S_HEAD(T, P) KB_S_TAIL
+
+// one 8-slot group of kb_insert2p, slots g..g+7 of kt / kp updated in place
+__device__ inline void kb_group8(float& t0, float& t1, float& t2, float& t3, float& t4, float& t5, float& t6, float& t7,
+                                 uint32_t& p0, uint32_t& p1, uint32_t& p2, uint32_t& p3, uint32_t& p4, uint32_t& p5,
+                                 uint32_t& p6, uint32_t& p7, float& pt0, uint32_t& pp0, float& pt1, uint32_t& pp1) {
+    float xt;
+    uint32_t xp;
+    uint64_t m0, m1;
+    asm("v_cmp_lt_f32_e64 %[m0], %[pt0], %[t0]\n\t"
+        "s_nop 1\n\t"
+        KB_S("%[t0]", "%[p0]", "%[t1]") KB_S("%[t1]", "%[p1]", "%[t2]") KB_S("%[t2]", "%[p2]", "%[t3]")
+        KB_S("%[t3]", "%[p3]", "%[t4]") KB_S("%[t4]", "%[p4]", "%[t5]") KB_S("%[t5]", "%[p5]", "%[t6]")
+        KB_S("%[t6]", "%[p6]", "%[t7]") KB_S_LAST("%[t7]", "%[p7]")
+        : [t0] "+v"(t0), [t1] "+v"(t1), [t2] "+v"(t2), [t3] "+v"(t3), [t4] "+v"(t4), [t5] "+v"(t5), [t6] "+v"(t6),
+          [t7] "+v"(t7), [p0] "+v"(p0), [p1] "+v"(p1), [p2] "+v"(p2), [p3] "+v"(p3), [p4] "+v"(p4), [p5] "+v"(p5),
+          [p6] "+v"(p6), [p7] "+v"(p7), [pt0] "+v"(pt0), [pp0] "+v"(pp0), [pt1] "+v"(pt1), [pp1] "+v"(pp1),
+          [xt] "=&v"(xt), [xp] "=&v"(xp), [m0] "=&s"(m0), [m1] "=&s"(m1));
+}
+
 template <int K>
 __device__ inline void kb_insert2p(float ta, float tb, uint32_t pk, float (&kt)[K], uint32_t (&kp)[K]) {
     constexpr int G = (K % GVRT_INSERT_GROUP == 0) ? GVRT_INSERT_GROUP : 4;
@@ -216,6 +262,14 @@ __device__ inline void kb_insert2p(float ta, float tb, uint32_t pk, float (&kt)[
 #pragma unroll
     for (int g = 0; g < K; g += G) {
         if (__builtin_amdgcn_ballot_w64(pt0 < kt[g + G - 1])) {
+#if GVRT_ASM_INSERT
+            if constexpr (G == 8) {
+                kb_group8(kt[g], kt[g + 1], kt[g + 2], kt[g + 3], kt[g + 4], kt[g + 5], kt[g + 6], kt[g + 7], kp[g],
+                          kp[g + 1], kp[g + 2], kp[g + 3], kp[g + 4], kp[g + 5], kp[g + 6], kp[g + 7], pt0, pp0, pt1,
+                          pp1);
+                continue;
+            }
+#endif
 #pragma unroll
             for (int i = g; i < g + G; ++i) {
                 const bool c0 = pt0 < kt[i];
@@ -473,7 +527,7 @@ typedef Node64 NodeT;
 typedef Bvh4Node NodeT;
 #endif
 
-template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK>
+template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK, bool SLACK>
 __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_render(const RenderArgs a, const NodeT* __restrict__ nodes_,
                                                 const RenderRec* __restrict__ recs_, const RenderRec* __restrict__ crecs_,
                                                 const uint4* __restrict__ aux_, const float* __restrict__ sh_,
@@ -721,7 +775,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
 #if GVRT_PK_BOX && !GVRT_ASM_NODE
                 const bool hit = box_hit_pk(nd.box[k], oinv, inv, tlo, tc, ent[k]);
 #else
-                const bool hit = box_hit(NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 1),
+                const bool hit = box_hit<SLACK>(NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 1),
                                          NODE_BOX(nd, k, 3), NODE_BOX(nd, k, 5), o, oinv, inv, tlo, tc, ent[k]);
 #endif
                 bal[k] = __builtin_amdgcn_ballot_w64(hit);  // compare result straight to an SGPR mask
@@ -1066,10 +1120,18 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
 #define KNODES a.nodes
 #endif
 #define KARGS KNODES, a.recs, a.crecs, a.aux, a.sh, a.view_inv, a.tiles, a.rgba8, a.rgba32f, a.ray_dirs, a.hit_counts, a.stats
-#define GVRT_LAUNCH(L, A, K, P)                                                                    \
-    do {                                                                                           \
-        if (a.stats) hipLaunchKernelGGL((k_render<L, A, K, true, P>), g, b, 0, c->stream, a, KARGS);  \
-        else hipLaunchKernelGGL((k_render<L, A, K, false, P>), g, b, 0, c->stream, a, KARGS);         \
+#define GVRT_LAUNCH_S(L, A, K, P, S)                                                                   \
+    do {                                                                                              \
+        if (a.stats) hipLaunchKernelGGL((k_render<L, A, K, true, P, S>), g, b, 0, c->stream, a, KARGS);  \
+        else hipLaunchKernelGGL((k_render<L, A, K, false, P, S>), g, b, 0, c->stream, a, KARGS);         \
+    } while (0)
+#define GVRT_LAUNCH(L, A, K, P) GVRT_LAUNCH_S(L, A, K, P, true)
+    // FAST packed kernels also come without the per-child box slack, used when the absolute box padding
+    // covers the plane rounding for this launch's cameras (RenderArgs::box_exact, set by render_impl)
+#define GVRT_LAUNCH_F(K)                                                                             \
+    do {                                                                                             \
+        if (a.box_exact) GVRT_LAUNCH_S(false, false, K, true, false);                                \
+        else GVRT_LAUNCH_S(false, false, K, true, true);                                             \
     } while (0)
     // packed payload needs record ids below 2^24 - 1 (id << 8 | q, all-ones = empty slot)
     // (GVRT_NO_PACK forces the unpacked path, which scenes of >= 2^24 - 1 survivors take, for testing)
@@ -1086,15 +1148,17 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
     } else {
         // FAST: the k-buffer depth only sets the number of traversal rounds, not the image
         switch (a.kfast) {
-            case 8: GVRT_LAUNCH(false, false, 8, true); break;
-            case 12: GVRT_LAUNCH(false, false, 12, true); break;
-            case 16: GVRT_LAUNCH(false, false, 16, true); break;
-            case 20: GVRT_LAUNCH(false, false, 20, true); break;
-            case 32: GVRT_LAUNCH(false, false, 32, true); break;
-            default: GVRT_LAUNCH(false, false, K_FAST_DEFAULT, true); break;
+            case 8: GVRT_LAUNCH_F(8); break;
+            case 12: GVRT_LAUNCH_F(12); break;
+            case 16: GVRT_LAUNCH_F(16); break;
+            case 20: GVRT_LAUNCH_F(20); break;
+            case 32: GVRT_LAUNCH_F(32); break;
+            default: GVRT_LAUNCH_F(K_FAST_DEFAULT); break;
         }
     }
 #undef GVRT_LAUNCH
+#undef GVRT_LAUNCH_F
+#undef GVRT_LAUNCH_S
     GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;
 }
