@@ -247,7 +247,17 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
                          "builder must be 0 (LBVH), 1 (PLOC), 2 (binned SAH, device) or 3 (binned SAH, host)");
     if (p->collapse > 1) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "collapse must be 0 (greedy) or 1 (SAH-optimal DP)");
     GVRT_HIP(c, hipSetDevice(c->device));
-    return gvrt_launch_build_accel(c, *p);
+    c->recs_ok = false;
+    gvrt_status s = gvrt_launch_build_accel(c, *p);
+    if (s) return s;
+    // leaf positions, kept aside for the launches whose records carry kernel-frame origins instead
+    gvrt_dfree(c, (void**)&c->d_leaf_p);
+    if (!c->split_cells && c->n_leaves) {
+        if ((s = gvrt_dalloc(c, (void**)&c->d_leaf_p, 12 * c->n_leaves))) return s;
+        if ((s = gvrt_launch_rec_prep(c, 0, nullptr))) return s;
+        GVRT_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    return GVRT_OK;
 }
 
 gvrt_status gvrt_build_accel(gvrt_handle c) { return gvrt_build_accel_ex(c, nullptr); }
@@ -534,6 +544,25 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
                       std::ldexp(omax, -20) <= c->box_pad_abs;  // also false for a NaN origin
     }
     a.kfast = p->kbuffer_depth ? p->kbuffer_depth : (uint32_t)K_FAST_DEFAULT;
+    // Single-origin FAST launches at the default depth read each leaf's kernel-frame origin ok from its record:
+    // one pass per launch writes ok = S^-1 R^T (o - p) in place of the position (k_rec_origin), instead of
+    // every leaf visit and composited hit of every wave recomputing it.  Other launches get the positions back.
+    {
+        bool one_origin = true;
+        for (uint32_t i = 1; i < ncams && one_origin; ++i)
+            one_origin = std::memcmp(view_inverse + 16ull * i + 12, view_inverse + 12, 12) == 0;
+        static const bool okrec_off = getenv("GVRT_OKREC") && getenv("GVRT_OKREC")[0] == '0';
+        const bool adaptive = (c->enc.opts & 1u) != 0;
+        a.okrec = !okrec_off && one_origin && p->mode == GVRT_MODE_FAST && a.kfast == (uint32_t)K_FAST_DEFAULT &&
+                  !adaptive && a.nrecs < 0xFFFFFFu && !getenv("GVRT_NO_PACK") && c->d_leaf_p && !c->split_cells;
+        if (a.okrec) {
+            if ((s = gvrt_launch_rec_prep(c, 1, view_inverse + 12))) return s;
+            c->recs_ok = true;
+        } else if (c->recs_ok) {
+            if ((s = gvrt_launch_rec_prep(c, 2, nullptr))) return s;
+            c->recs_ok = false;
+        }
+    }
     if (a.kfast != 8 && a.kfast != 12 && a.kfast != 16 && a.kfast != 20 && a.kfast != 24 && a.kfast != 32)
         return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "kbuffer_depth must be 0, 8, 12, 16, 20, 24 or 32");
     uint64_t nwork = total_tiles;

@@ -128,6 +128,7 @@ struct RenderArgs {
     uint32_t ray_dirs_layout;
     uint32_t packed;
     uint32_t kfast;  // FAST-mode k-buffer depth (8, 12, 16, 24)
+    uint32_t okrec;      // records hold kernel-frame origins for this launch's single camera origin
     uint32_t box_exact;  // box padding covers the plane rounding for these cameras: no per-child slack
     float grid_min[3];  // split grid (SplitBLAS analogue): origin and 1 / cell size
     float grid_inv;

@@ -53,6 +53,9 @@ struct gvrt_context {
     uint64_t n_nodes4 = 0;
     gvrt::Node64* d_nodes64 = nullptr;  // GVRT_NODE64 builds: the compressed copy the render kernel reads
     uint32_t* d_leaf_src = nullptr;  // leaf -> compaction index
+    float* d_leaf_p = nullptr;       // leaf positions (3 per leaf): d_recs keeps ok in their place while recs_ok
+    bool recs_ok = false;            // d_recs hold kernel-frame origins for rec_origin (k_rec_origin)
+    float rec_origin[3] = {0, 0, 0};
     uint64_t n_leaves = 0;           // BVH leaves: the survivors, or their split pieces
     uint32_t* d_leaf_aux = nullptr;  // split: per leaf {proxy, cell, proxy's cell range lo, hi} (uint4); else null
     uint32_t split_cells = 0;        // grid cells on the longest axis (0: no split)
@@ -126,5 +129,7 @@ gvrt_status gvrt_sah_build_device(gvrt_context* c, uint64_t m, const float* lbox
 // gvrt_render.hip
 gvrt_status gvrt_launch_render_mode(gvrt_context* c, const gvrt::RenderArgs& a, uint64_t nwaves, bool literal);
 gvrt_status gvrt_launch_tile_order(gvrt_context* c);
+// record preparation: op 0 save leaf positions, 1 write kernel-frame origins for o, 2 restore positions
+gvrt_status gvrt_launch_rec_prep(gvrt_context* c, int op, const float* o);
 gvrt_status gvrt_launch_unpack(gvrt_context* c, const void* packed, const uint32_t* tiles,
                                uint64_t ntiles, uint32_t width, uint32_t height, void* frame);

@@ -293,15 +293,33 @@ __device__ inline void kb_insert2p(float ta, float tb, uint32_t pk, float (&kt)[
 // Written with explicit fmaf and contraction off: the insert-time and composite-time evaluations of
 // kernel_frame / particle_alpha must round identically, and the backend otherwise fuses mul+add pairs
 // differently at each inlined site (SLP-packed v_pk_fma_f32 at one, scalar mul/sub at the other).
-__device__ inline void kernel_frame(const RenderRec& rec, f3 o, f3 d, f3& ok, f3& dk) {
+__device__ inline f3 kernel_org(const RenderRec& rec, f3 o) {
 #pragma clang fp contract(off)
     const float ex = o.x - rec.px, ey = o.y - rec.py, ez = o.z - rec.pz;
-    ok = mk3(fmaf(rec.c2x, ez, fmaf(rec.c1x, ey, rec.c0x * ex)) * rec.isx,
-             fmaf(rec.c2y, ez, fmaf(rec.c1y, ey, rec.c0y * ex)) * rec.isy,
-             fmaf(rec.c2z, ez, fmaf(rec.c1z, ey, rec.c0z * ex)) * rec.isz);
-    dk = mk3(fmaf(rec.c2x, d.z, fmaf(rec.c1x, d.y, rec.c0x * d.x)) * rec.isx,
-             fmaf(rec.c2y, d.z, fmaf(rec.c1y, d.y, rec.c0y * d.x)) * rec.isy,
-             fmaf(rec.c2z, d.z, fmaf(rec.c1z, d.y, rec.c0z * d.x)) * rec.isz);
+    return mk3(fmaf(rec.c2x, ez, fmaf(rec.c1x, ey, rec.c0x * ex)) * rec.isx,
+               fmaf(rec.c2y, ez, fmaf(rec.c1y, ey, rec.c0y * ex)) * rec.isy,
+               fmaf(rec.c2z, ez, fmaf(rec.c1z, ey, rec.c0z * ex)) * rec.isz);
+}
+__device__ inline f3 kernel_dir(const RenderRec& rec, f3 d) {
+#pragma clang fp contract(off)
+    return mk3(fmaf(rec.c2x, d.z, fmaf(rec.c1x, d.y, rec.c0x * d.x)) * rec.isx,
+               fmaf(rec.c2y, d.z, fmaf(rec.c1y, d.y, rec.c0y * d.x)) * rec.isy,
+               fmaf(rec.c2z, d.z, fmaf(rec.c1z, d.y, rec.c0z * d.x)) * rec.isz);
+}
+// OKREC: the launch's records carry the kernel-frame origin ok in place of the position (k_rec_origin
+// wrote it for this launch's single camera origin, with kernel_org: the same bits as computing it here)
+__device__ inline float to_vgpr(float x) {  // a scalar-loaded record field copied to a VGPR: not kept live in
+    float r;                                  // SGPRs past the leaf test (that spilled SGPRs)
+    asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+    return r;
+}
+// SREC: rec was fetched by scalar loads (leaf visits), else per lane (composite)
+template <bool OKREC, bool SREC = false>
+__device__ inline void kernel_frame(const RenderRec& rec, f3 o, f3 d, f3& ok, f3& dk) {
+    if constexpr (OKREC && SREC) ok = mk3(to_vgpr(rec.px), to_vgpr(rec.py), to_vgpr(rec.pz));
+    else if constexpr (OKREC) ok = mk3(rec.px, rec.py, rec.pz);
+    else ok = kernel_org(rec, o);
+    dk = kernel_dir(rec, d);
 }
 
 __device__ inline float len2(f3 v) {
@@ -527,7 +545,7 @@ typedef Node64 NodeT;
 typedef Bvh4Node NodeT;
 #endif
 
-template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK, bool SLACK>
+template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK, bool SLACK, bool OKREC>
 __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_render(const RenderArgs a, const NodeT* __restrict__ nodes_,
                                                 const RenderRec* __restrict__ recs_, const RenderRec* __restrict__ crecs_,
                                                 const uint4* __restrict__ aux_, const float* __restrict__ sh_,
@@ -841,7 +859,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                         if constexpr (STATS) ++l_leaves;
                         // ---- leaf: response (processHit's math) + analytic icosahedron clip
                         f3 ok, dk;
-                        kernel_frame(rec, o, d, ok, dk);
+                        kernel_frame<OKREC, true>(rec, o, d, ok, dk);
                         // Conservative pre-reject: gres > hitMinGaussianResponse needs the squared line
                         // distance gd = |dk x ok|^2 / |dk|^2 below sqrt(ln(minResponse)/S) (a.gpre carries a
                         // 1e-3 margin), so most proxies are rejected without the sqrt / exp below.
@@ -959,7 +977,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                             // processHit re-evaluates the response of the hit particle (per-lane record load)
                             const RenderRec rec = crecs_[hid];
                             f3 ok, dk;
-                            kernel_frame(rec, o, d, ok, dk);
+                            kernel_frame<OKREC>(rec, o, d, ok, dk);
                             const float l2 = len2(dk);
                             hacc = particle_alpha(ok, dk, l2, rec.density, a.min_response, a.alpha_min, halpha);
                         } else {
@@ -1120,18 +1138,18 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
 #define KNODES a.nodes
 #endif
 #define KARGS KNODES, a.recs, a.crecs, a.aux, a.sh, a.view_inv, a.tiles, a.rgba8, a.rgba32f, a.ray_dirs, a.hit_counts, a.stats
-#define GVRT_LAUNCH_S(L, A, K, P, S)                                                                   \
-    do {                                                                                              \
-        if (a.stats) hipLaunchKernelGGL((k_render<L, A, K, true, P, S>), g, b, 0, c->stream, a, KARGS);  \
-        else hipLaunchKernelGGL((k_render<L, A, K, false, P, S>), g, b, 0, c->stream, a, KARGS);         \
+#define GVRT_LAUNCH_SO(L, A, K, P, S, O)                                                                  \
+    do {                                                                                                  \
+        if (a.stats) hipLaunchKernelGGL((k_render<L, A, K, true, P, S, O>), g, b, 0, c->stream, a, KARGS);   \
+        else hipLaunchKernelGGL((k_render<L, A, K, false, P, S, O>), g, b, 0, c->stream, a, KARGS);          \
     } while (0)
-#define GVRT_LAUNCH(L, A, K, P) GVRT_LAUNCH_S(L, A, K, P, true)
+#define GVRT_LAUNCH(L, A, K, P) GVRT_LAUNCH_SO(L, A, K, P, true, false)
     // FAST packed kernels also come without the per-child box slack, used when the absolute box padding
     // covers the plane rounding for this launch's cameras (RenderArgs::box_exact, set by render_impl)
 #define GVRT_LAUNCH_F(K)                                                                             \
     do {                                                                                             \
-        if (a.box_exact) GVRT_LAUNCH_S(false, false, K, true, false);                                \
-        else GVRT_LAUNCH_S(false, false, K, true, true);                                             \
+        if (a.box_exact) GVRT_LAUNCH_SO(false, false, K, true, false, false);                        \
+        else GVRT_LAUNCH_SO(false, false, K, true, true, false);                                     \
     } while (0)
     // packed payload needs record ids below 2^24 - 1 (id << 8 | q, all-ones = empty slot)
     // (GVRT_NO_PACK forces the unpacked path, which scenes of >= 2^24 - 1 survivors take, for testing)
@@ -1153,12 +1171,18 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
             case 16: GVRT_LAUNCH_F(16); break;
             case 20: GVRT_LAUNCH_F(20); break;
             case 32: GVRT_LAUNCH_F(32); break;
-            default: GVRT_LAUNCH_F(K_FAST_DEFAULT); break;
+            default:
+                // the default depth also reads kernel-frame origins from the records when render_impl
+                // prepared them for a single-origin launch (RenderArgs::okrec)
+                if (a.okrec && a.box_exact) GVRT_LAUNCH_SO(false, false, K_FAST_DEFAULT, true, false, true);
+                else if (a.okrec) GVRT_LAUNCH_SO(false, false, K_FAST_DEFAULT, true, true, true);
+                else GVRT_LAUNCH_F(K_FAST_DEFAULT);
+                break;
         }
     }
 #undef GVRT_LAUNCH
 #undef GVRT_LAUNCH_F
-#undef GVRT_LAUNCH_S
+#undef GVRT_LAUNCH_SO
     GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;
 }
@@ -1258,6 +1282,47 @@ gvrt_status gvrt_launch_tile_order(gvrt_context* c) {
     GVRT_HIP(c, hipGetLastError());
     c->ord_parity = 1 - p;
     c->ord_ready = true;
+    return GVRT_OK;
+}
+
+// Per-launch record preparation for single-origin FAST launches: each leaf record's position is replaced by
+// its kernel-frame origin ok = S^-1 R^T (o - p) (kernel_org, the arithmetic the render kernel would do per
+// leaf visit and per composited hit); k_rec_restore puts the positions back for launches that need them.
+__global__ __launch_bounds__(256) void k_rec_origin(uint64_t m, const float* __restrict__ leaf_p, RenderRec* recs,
+                                                    float ox, float oy, float oz) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    RenderRec r = recs[i];
+    r.px = leaf_p[3 * i];
+    r.py = leaf_p[3 * i + 1];
+    r.pz = leaf_p[3 * i + 2];
+    const f3 ok = kernel_org(r, mk3(ox, oy, oz));
+    float4* w = reinterpret_cast<float4*>(recs + i);
+    w[0] = make_float4(ok.x, ok.y, ok.z, r.density);
+}
+__global__ __launch_bounds__(256) void k_rec_restore(uint64_t m, const float* __restrict__ leaf_p, RenderRec* recs) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    recs[i].px = leaf_p[3 * i];
+    recs[i].py = leaf_p[3 * i + 1];
+    recs[i].pz = leaf_p[3 * i + 2];
+}
+__global__ __launch_bounds__(256) void k_rec_save(uint64_t m, const RenderRec* __restrict__ recs, float* leaf_p) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    leaf_p[3 * i] = recs[i].px;
+    leaf_p[3 * i + 1] = recs[i].py;
+    leaf_p[3 * i + 2] = recs[i].pz;
+}
+
+gvrt_status gvrt_launch_rec_prep(gvrt_context* c, int op, const float* o) {
+    const uint64_t m = c->n_leaves;
+    if (!m || !c->d_leaf_p) return GVRT_OK;
+    const dim3 g((unsigned)((m + 255) / 256)), b(256);
+    if (op == 0) hipLaunchKernelGGL(k_rec_save, g, b, 0, c->stream, m, c->d_recs, c->d_leaf_p);
+    else if (op == 1) hipLaunchKernelGGL(k_rec_origin, g, b, 0, c->stream, m, c->d_leaf_p, c->d_recs, o[0], o[1], o[2]);
+    else hipLaunchKernelGGL(k_rec_restore, g, b, 0, c->stream, m, c->d_leaf_p, c->d_recs);
+    GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;
 }
 

@@ -184,6 +184,34 @@ def test_cost_ordered_dispatch_changes_no_pixel(gv, config1):
                                           first["rgba32f"][0][8 * ty:8 * ty + 8, 8 * tx:8 * tx + 8])
 
 
+def test_record_origin_prep_changes_no_pixel(gv, config1):
+    """Single-origin FAST launches read each leaf's kernel-frame origin from its record (k_rec_origin writes it
+    per launch in place of the position; other launches get the positions back, k_rec_restore).  Frames agree
+    bit for bit with the same cameras rendered by a multi-origin launch (positions path), across mode
+    switches, and for queued launches with different origins (each launch's records prepared in stream order)."""
+    W, H = 64, 48
+    vi3, pi3 = gv.camera.lightfield_grid_rig((0.0, 0.0, 3.0), (0.0, 0.0, 0.0), nx=3, ny=1, spacing=0.3,
+                                              aspect=gv.camera.aspect_ratio(W, H))
+    cams = [vi3[16 * k:16 * (k + 1)] for k in range(3)]
+    with gv.Renderer(0) as r:
+        r.prepare(config1)
+        multi = r.render(vi3, pi3, W, H, ncams=3)["rgba32f"]          # three origins: positions
+        single = [r.render(v, pi3, W, H)["rgba32f"][0] for v in cams]  # one origin each: prepared records
+        for k in range(3):
+            np.testing.assert_array_equal(single[k], multi[k])
+        lit = r.render(cams[1], pi3, W, H, mode=gv.MODE_LITERAL)["rgba32f"]  # LITERAL: positions restored
+        np.testing.assert_array_equal(r.render(cams[1], pi3, W, H)["rgba32f"][0], single[1])
+        np.testing.assert_array_equal(r.render(cams[1], pi3, W, H, mode=gv.MODE_LITERAL)["rgba32f"], lit)
+        # queued launches alternating between two origins, device outputs
+        import torch
+        outs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(4)]
+        for i, o in enumerate(outs):
+            r.render_device(cams[i % 2 * 2], pi3, W, H, rgba32f_ptr=o.data_ptr(), async_=True)
+        r.sync()
+        for i, o in enumerate(outs):
+            np.testing.assert_array_equal(o.cpu().numpy(), single[i % 2 * 2])
+
+
 def test_caller_stream_queued_split_frame(gv, config1):
     """The multi-GPU exchange's device-side pipeline on one GPU: renders queued (gvrt_render_async) on a
     caller stream (gvrt_set_stream), each rank part of a tile-split frame rendered tile-packed, then all parts
