@@ -51,6 +51,15 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 #ifndef GVRT_PK_BOX
 #define GVRT_PK_BOX 0  // packed-FMA box test: measured 3 % slower (more VGPRs for the broadcast pairs)
 #endif
+#ifndef GVRT_SH_UNCOND
+#define GVRT_SH_UNCOND 1
+#endif
+#ifndef GVRT_SH_EARLY
+#define GVRT_SH_EARLY 6  // float4 SH loads consumed before the accept branch (multiple of 3, <= 12)
+#endif
+#ifndef GVRT_HM_ASM
+#define GVRT_HM_ASM 1
+#endif
 #ifndef GVRT_SH_PREFETCH
 #define GVRT_SH_PREFETCH 1
 #endif
@@ -503,6 +512,14 @@ __device__ inline int lane_now() {
     return r;
 }
 
+// bit if the lane mask is non-empty, on the SALU (left to the compiler one of the four went through a
+// v_cndmask + v_readfirstlane round trip on every node visit)
+__device__ inline uint32_t nz_bit(uint64_t m, uint32_t bit) {
+    uint32_t r;
+    asm("s_cmp_lg_u64 %1, 0\n\ts_cselect_b32 %0, %2, 0" : "=s"(r) : "s"(m), "s"(bit) : "scc");
+    return r;
+}
+
 __device__ inline uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ inline float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
@@ -807,7 +824,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
             // (the entry-distance sort below costs ~100)
             uint32_t hm = 0;
 #pragma unroll
-            for (int k = 0; k < BVH_W; ++k) hm |= bal[k] ? (1u << k) : 0u;
+            for (int k = 0; k < BVH_W; ++k) hm |= GVRT_HM_ASM ? nz_bit(bal[k], 1u << k) : (bal[k] ? (1u << k) : 0u);
             if constexpr (STATS) w_dead += hm == 0 ? 1u : 0u;
             const uint32_t inner = uni(NODE_PAD(nd, 1));
             uint32_t leafmask = hm & ~inner;
@@ -965,7 +982,9 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                         hid = PACK ? (kid[j] >> 8) : kid[j];
 #if GVRT_SH_PREFETCH
                         // the SH address needs only the id: issue all 12 loads with the record's, one
-                        // memory round trip per hit instead of one per dependent chunk
+                        // memory round trip per hit instead of one per dependent chunk (with GVRT_SH_UNCOND the
+                        // first GVRT_SH_EARLY of them are consumed unconditionally, so they are not sunk behind
+                        // the accept branch; all 12 early spilled VGPRs)
                         float4 shv[12];
                         {
                             const float4* s4 = reinterpret_cast<const float4*>(sh_ + 48ull * hid);
@@ -985,12 +1004,26 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                             hacc = ka[j] > 0.0f;
                         }
                         GVRT_TRACE_REC(trace_on, 2, hid, kt[j], halpha, T, hacc ? 1.0f : 0.0f, rounds);
+                        float er = 0.f, eg = 0.f, eb = 0.f;  // SH terms of the first GVRT_SH_EARLY / 3 chunks
+#if GVRT_SH_PREFETCH
+                        if constexpr (GVRT_SH_UNCOND && PACK) {
+#pragma unroll
+                            for (int q = 0; q < GVRT_SH_EARLY / 3; ++q) {
+                                const float4 v0 = shv[3 * q], v1 = shv[3 * q + 1], v2 = shv[3 * q + 2];
+                                const float4 bq = s_basis[wid][q][lane];
+                                er += bq.x * v0.x; eg += bq.x * v0.y; eb += bq.x * v0.z;
+                                er += bq.y * v0.w; eg += bq.y * v1.x; eb += bq.y * v1.y;
+                                er += bq.z * v1.z; eg += bq.z * v1.w; eb += bq.z * v2.x;
+                                er += bq.w * v2.y; eg += bq.w * v2.z; eb += bq.w * v2.w;
+                            }
+                        }
+#endif
                         if (hacc) {
                             const float weight = halpha * T;
-                            float rr = 0.f, rg = 0.f, rb = 0.f;
+                            float rr = er, rg = eg, rb = eb;
 #if GVRT_SH_PREFETCH
 #pragma unroll
-                            for (int q = 0; q < 4; ++q) {
+                            for (int q = (GVRT_SH_UNCOND && PACK) ? GVRT_SH_EARLY / 3 : 0; q < 4; ++q) {
                                 const float4 v0 = shv[3 * q], v1 = shv[3 * q + 1], v2 = shv[3 * q + 2];
 #else
                             const float4* s4 = reinterpret_cast<const float4*>(sh_ + 48ull * hid);
