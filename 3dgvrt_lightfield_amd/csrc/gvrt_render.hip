@@ -73,6 +73,9 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 #ifndef GVRT_TCUT
 #define GVRT_TCUT 1
 #endif
+#ifndef GVRT_TCUT_GROUPS
+#define GVRT_TCUT_GROUPS 0
+#endif
 #ifndef GVRT_VSTACK
 #define GVRT_VSTACK 0
 #endif
@@ -916,11 +919,28 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                                     if (__builtin_amdgcn_ballot_w64(qtot >= qneed)) {
                                     uint32_t qs = 0;
                                     float tt = INF_DIST;
+#if GVRT_TCUT_GROUPS
+                                    // in 8-slot groups; slots are sorted, so once every walking lane has its cut
+                                    // the later groups cannot lower it
+                                    bool more = true;
+#pragma unroll
+                                    for (int g = 0; g < KB; g += 8) {
+                                        if (more) {
+#pragma unroll
+                                            for (int i = g; i < (g + 8 < KB ? g + 8 : KB); ++i) {
+                                                qs += kid[i] & 0xFFu;
+                                                tt = fminf(tt, qs >= qneed ? kt[i] : INF_DIST);
+                                            }
+                                            more = __builtin_amdgcn_ballot_w64(tt == INF_DIST && qtot >= qneed) != 0;
+                                        }
+                                    }
+#else
 #pragma unroll
                                     for (int i = 0; i < KB; ++i) {
                                         qs += kid[i] & 0xFFu;
                                         tt = fminf(tt, qs >= qneed ? kt[i] : INF_DIST);
                                     }
+#endif
                                     tcut = fminf(tcut, tt);
                                     }
 #endif
