@@ -248,8 +248,10 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
     if (p->collapse > 1) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "collapse must be 0 (greedy) or 1 (SAH-optimal DP)");
     GVRT_HIP(c, hipSetDevice(c->device));
     c->recs_ok = false;
+    gvrt_dfree(c, (void**)&c->d_nodes4x8);
     gvrt_status s = gvrt_launch_build_accel(c, *p);
     if (s) return s;
+    if ((s = gvrt_launch_node_octants(c))) return s;
     // leaf positions, kept aside for the launches whose records carry kernel-frame origins instead
     gvrt_dfree(c, (void**)&c->d_leaf_p);
     if (!c->split_cells && c->n_leaves) {
@@ -491,6 +493,9 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
     for (int k = 0; k < 3; ++k) a.grid_min[k] = c->grid_min[k];
     a.grid_inv = c->grid_inv;
     a.nodes = c->d_nodes4;
+    static const bool oct_off = getenv("GVRT_OCT_NODES") && getenv("GVRT_OCT_NODES")[0] == '0';
+    a.nodes8 = oct_off ? nullptr : c->d_nodes4x8;
+    a.nodes8_stride = c->n_nodes4;
     a.nodes64 = c->d_nodes64;
     a.nrecs = (uint32_t)c->m;
     // the render kernel addresses leaf records (64 B) and 4-wide nodes (128 B) by 32-bit byte offsets

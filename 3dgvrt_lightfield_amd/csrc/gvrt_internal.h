@@ -51,6 +51,7 @@ struct gvrt_context {
     gvrt::BvhNode* d_nodes = nullptr;   // binary LBVH (kept for diagnostics)
     gvrt::Bvh4Node* d_nodes4 = nullptr; // 4-wide collapse traversed by the render kernel
     uint64_t n_nodes4 = 0;
+    gvrt::Bvh4Node* d_nodes4x8 = nullptr;  // 8 octant copies of d_nodes4 (planes in near / far order)
     gvrt::Node64* d_nodes64 = nullptr;  // GVRT_NODE64 builds: the compressed copy the render kernel reads
     uint32_t* d_leaf_src = nullptr;  // leaf -> compaction index
     float* d_leaf_p = nullptr;       // leaf positions (3 per leaf): d_recs keeps ok in their place while recs_ok
@@ -131,5 +132,7 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const gvrt::RenderArgs& a, 
 gvrt_status gvrt_launch_tile_order(gvrt_context* c);
 // record preparation: op 0 save leaf positions, 1 write kernel-frame origins for o, 2 restore positions
 gvrt_status gvrt_launch_rec_prep(gvrt_context* c, int op, const float* o);
+// the 8 octant copies of the 4-wide nodes (d_nodes4x8)
+gvrt_status gvrt_launch_node_octants(gvrt_context* c);
 gvrt_status gvrt_launch_unpack(gvrt_context* c, const void* packed, const uint32_t* tiles,
                                uint64_t ntiles, uint32_t width, uint32_t height, void* frame);

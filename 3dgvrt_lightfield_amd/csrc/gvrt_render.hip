@@ -73,6 +73,9 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 #ifndef GVRT_TCUT
 #define GVRT_TCUT 1
 #endif
+#ifndef GVRT_DIAG_PAIRS
+#define GVRT_DIAG_PAIRS 0
+#endif
 #ifndef GVRT_TCUT_GROUPS
 #define GVRT_TCUT_GROUPS 0
 #endif
@@ -131,6 +134,20 @@ __device__ inline bool box_hit(float lx, float ly, float lz, float hx, float hy,
     // absolute box padding of gvrt_enclose.hip (2^-18 x the scene's position bound) covers the rounding
     // of these FMA-form planes, (2|lo| + 3|o|) * 2^-24 per plane in world units, as long as the ray
     // origin lies within 4x that bound (render_impl chooses the variant per launch).
+    if constexpr (SLACK) return tn <= tf + 2e-6f * fabsf(tf);
+    else return tn <= tf;
+}
+
+// Slab test on planes stored in (near, far) order for the ray's octant (octant copies of the nodes): the
+// same plane values as box_hit's, and its min / max pairs are the near / far planes, so no pair is needed
+template <bool SLACK>
+__device__ inline bool box_hit_nf(float nx, float ny, float nz, float fx, float fy, float fz, f3 oinv, f3 inv, float t0,
+                                  float t1) {
+    const float an = fmaf(nx, inv.x, -oinv.x), af = fmaf(fx, inv.x, -oinv.x);
+    const float bn = fmaf(ny, inv.y, -oinv.y), bf = fmaf(fy, inv.y, -oinv.y);
+    const float cn = fmaf(nz, inv.z, -oinv.z), cf = fmaf(fz, inv.z, -oinv.z);
+    const float tn = fmaxf(fmaxf(t0, an), fmaxf(bn, cn));
+    const float tf = fminf(fminf(t1, af), fminf(bf, cf));
     if constexpr (SLACK) return tn <= tf + 2e-6f * fabsf(tf);
     else return tn <= tf;
 }
@@ -675,6 +692,20 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
     uint32_t w_rounds = 0, w_late = 0;  // traversal rounds of this wave; node visits after the first round
     [[maybe_unused]] const uint64_t cyc_start = STATS ? __builtin_amdgcn_s_memtime() : 0;
     bool active = valid && a.nrecs > 0 && (fmaxf(0.0f, tminb - EPS_T) <= tmaxb) && (1.0f > a.min_transmittance);
+#if !GVRT_NODE64
+    // a wave whose active rays share one direction octant reads that octant's node copy (planes in near / far
+    // order, box_hit_nf); waves straddling an axis sign (a few tiles on the lines where a direction component
+    // changes sign) read the plain nodes
+    bool octw = false;
+    const Bvh4Node* __restrict__ nbase = nodes_;
+    if (a.nodes8) {
+        const uint32_t oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
+        const uint64_t am = __builtin_amdgcn_ballot_w64(active);
+        const uint32_t oct0 = (uint32_t)__builtin_amdgcn_readlane((int)oct, am ? (int)__builtin_ctzll(am) : 0);
+        octw = __builtin_amdgcn_ballot_w64(active && oct != oct0) == 0;
+        if (octw) nbase = a.nodes8 + a.nodes8_stride * oct0;
+    }
+#endif
 
     static_assert(!(LITERAL && PACK), "LITERAL keeps rejected crossings: unpacked k-buffer");
     float kt[KB];
@@ -762,13 +793,13 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
             [[maybe_unused]] uint64_t t_node0 = 0;
             if constexpr (STATS) {
                 ++w_nodes;
-                w_late += w_rounds > 1 ? 1u : 0u;
+                if constexpr (!GVRT_DIAG_PAIRS) w_late += w_rounds > 1 ? 1u : 0u;
                 t_node0 = __builtin_amdgcn_s_memtime();  // the node phase includes the fetch
             }
 #if GVRT_NODE64
             const sv16 nd = load_node64_at(nodes_, unii(cur));  // whole node: one s_load_dwordx16
 #elif GVRT_SOFF
-            const NodeS nd = load_node_at(nodes_, unii(cur));  // whole node: 2x s_load_dwordx16 (4-wide)
+            const NodeS nd = load_node_at(nbase, unii(cur));  // whole node: 2x s_load_dwordx16 (4-wide)
 #else
             const NodeS nd = load_node(nodes_ + unii(cur));  // whole node: 2x s_load_dwordx16 (4-wide)
 #endif
@@ -807,7 +838,19 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
             if (im) {
                 const bool rev = (rsign >> ((meta >> 8) & 3u)) & 1u;
 #else
-            // (a per-octant min/max-free box test measured within noise: +0.7 %, 9 code copies)
+            // (a per-octant min/max-free box test as 8 template copies of the loop measured within noise: +0.7 %;
+            // the octant node copies below keep one code path for all octants)
+            if (octw) {
+                // (an opaque copy of 1/d: otherwise the first child's plane FMAs, common to both tests, are hoisted
+                // above the branch and every min / max input after it gets a canonicalising v_max)
+                f3 iv = inv;
+                asm("" : "+v"(iv.x), "+v"(iv.y), "+v"(iv.z));
+#pragma unroll
+                for (int k = 0; k < BVH_W; ++k)
+                    bal[k] = __builtin_amdgcn_ballot_w64(
+                        box_hit_nf<SLACK>(NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 1),
+                                          NODE_BOX(nd, k, 3), NODE_BOX(nd, k, 5), oinv, iv, tlo, tc));
+            } else {
 #pragma unroll
             for (int k = 0; k < BVH_W; ++k) {
 #if GVRT_PK_BOX && !GVRT_ASM_NODE
@@ -819,6 +862,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                 bal[k] = __builtin_amdgcn_ballot_w64(hit);  // compare result straight to an SGPR mask
                 if constexpr (!GVRT_SOFF) bal[k] &= amask;
             }
+            }
             int32_t ch[BVH_W];
 #pragma unroll
             for (int k = 0; k < BVH_W; ++k) ch[k] = unii(NODE_CHILD(nd, k));
@@ -828,9 +872,25 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
             uint32_t hm = 0;
 #pragma unroll
             for (int k = 0; k < BVH_W; ++k) hm |= GVRT_HM_ASM ? nz_bit(bal[k], 1u << k) : (bal[k] ? (1u << k) : 0u);
-            if constexpr (STATS) w_dead += hm == 0 ? 1u : 0u;
+            if constexpr (STATS && !GVRT_DIAG_PAIRS) w_dead += hm == 0 ? 1u : 0u;
             const uint32_t inner = uni(NODE_PAD(nd, 1));
             uint32_t leafmask = hm & ~inner;
+#if GVRT_DIAG_PAIRS
+            // diagnostic (STATS build): w_dead counts node visits whose hit leaf children's (leaf, lane) pairs fit
+            // fewer 64-lane passes than leaves; w_late sums the leaf passes such compaction would save
+            if constexpr (STATS) {
+                uint32_t nl = 0, np = 0;
+#pragma unroll
+                for (int k = 0; k < BVH_W; ++k)
+                    if ((leafmask >> k) & 1u) {
+                        ++nl;
+                        np += (uint32_t)__builtin_popcountll(bal[k]);
+                    }
+                const uint32_t passes = (np + 63) / 64;
+                w_dead += (nl >= 2 && passes < nl) ? 1u : 0u;
+                w_late += nl - passes;
+            }
+#endif
             uint32_t im = hm & inner;
             int32_t next = -1;
             auto chsel = [&](int k) { return GVRT_PICK(ch, k); };
@@ -1379,6 +1439,47 @@ gvrt_status gvrt_launch_rec_prep(gvrt_context* c, int op, const float* o) {
     else hipLaunchKernelGGL(k_rec_restore, g, b, 0, c->stream, m, c->d_leaf_p, c->d_recs);
     GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;
+}
+
+// The 8 octant copies of the 4-wide nodes: copy o stores, for every axis a with bit a of o set (rays along
+// -a), each child box's (hi, lo) in the (lo, hi) slots, so a wave of octant o finds its near planes in the lo
+// slots.  Empty slots hold EMPTY_BOX in all six and stay unhittable; children and flags are copied unchanged.
+__global__ __launch_bounds__(256) void k_node_octants(uint64_t n, const Bvh4Node* __restrict__ src,
+                                                      Bvh4Node* __restrict__ dst) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 8 * n) return;
+    const uint32_t o = (uint32_t)(i / n);
+    Bvh4Node nd = src[i % n];
+#pragma unroll
+    for (int k = 0; k < BVH_W; ++k)
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax)
+            if ((o >> ax) & 1u) {
+                const float lo = nd.box[k][2 * ax];
+                nd.box[k][2 * ax] = nd.box[k][2 * ax + 1];
+                nd.box[k][2 * ax + 1] = lo;
+            }
+    dst[i] = nd;
+}
+
+gvrt_status gvrt_launch_node_octants(gvrt_context* c) {
+#if GVRT_NODE64 || GVRT_BVH_W != 4
+    (void)c;
+    return GVRT_OK;
+#else
+    const uint64_t n = c->n_nodes4;
+    if (!n || !c->d_nodes4) return GVRT_OK;
+    // 8 x the node array (0.46 GB at 1 M Gaussians); when it does not fit, waves read the plain nodes
+    if (gvrt_dalloc(c, (void**)&c->d_nodes4x8, 8 * n * sizeof(Bvh4Node)) != GVRT_OK) {
+        c->d_nodes4x8 = nullptr;
+        c->err.clear();
+        return GVRT_OK;
+    }
+    hipLaunchKernelGGL(k_node_octants, dim3((unsigned)((8 * n + 255) / 256)), dim3(256), 0, c->stream, n, c->d_nodes4,
+                       c->d_nodes4x8);
+    GVRT_HIP(c, hipGetLastError());
+    return GVRT_OK;
+#endif
 }
 
 gvrt_status gvrt_launch_unpack(gvrt_context* c, const void* packed, const uint32_t* tiles, uint64_t ntiles,
