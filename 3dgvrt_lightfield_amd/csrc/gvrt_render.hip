@@ -152,6 +152,43 @@ __device__ inline bool box_hit_nf(float nx, float ny, float nz, float fx, float 
     else return tn <= tf;
 }
 
+// Octant-node plane distances by packed FMA: one v_pk_fma_f32 gives an axis's (near, far) pair from the node's
+// SGPR pair, with the lane's 1/d and o/d broadcast to both halves by op_sel / op_sel_hi (negated by neg_lo /
+// neg_hi): the same fma(plane, 1/d, -o/d) values as box_hit_nf's six v_fma_f32, in three instructions.
+// The ray's constants ride in three VGPR pairs: (1/dx, 1/dy), (ox/dx, oy/dy), (1/dz, oz/dz).
+#ifndef GVRT_PK_NF
+#define GVRT_PK_NF 0  // measured within noise to +1 % slower (latency-bound node chain)
+#endif
+typedef float pf2 __attribute__((ext_vector_type(2)));
+__device__ inline pf2 pk_plane_x(pf2 box, pf2 ixy, pf2 oxy) {
+    pf2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[1,0,0] neg_lo:[0,0,1] neg_hi:[0,0,1]"
+        : "=v"(r) : "s"(box), "v"(ixy), "v"(oxy));
+    return r;
+}
+__device__ inline pf2 pk_plane_y(pf2 box, pf2 ixy, pf2 oxy) {
+    pf2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,1] op_sel_hi:[1,1,1] neg_lo:[0,0,1] neg_hi:[0,0,1]"
+        : "=v"(r) : "s"(box), "v"(ixy), "v"(oxy));
+    return r;
+}
+__device__ inline pf2 pk_plane_z(pf2 box, pf2 izo) {
+    pf2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] neg_lo:[0,0,1] neg_hi:[0,0,1]"
+        : "=v"(r) : "s"(box), "v"(izo));
+    return r;
+}
+template <bool SLACK>
+__device__ inline bool box_hit_pk_nf(pf2 bx, pf2 by, pf2 bz, pf2 ixy, pf2 oxy, pf2 izo, float t0, float t1) {
+    const pf2 X = pk_plane_x(bx, ixy, oxy), Y = pk_plane_y(by, ixy, oxy), Z = pk_plane_z(bz, izo);
+    // max / min in asm too: fmaxf / fminf on asm outputs get a canonicalising v_max per input (4 per box)
+    float tn, tf;
+    asm("v_max3_f32 %0, %1, %2, %3\n\tv_max_f32 %0, %0, %4" : "=&v"(tn) : "v"(t0), "v"(X.x), "v"(Y.x), "v"(Z.x));
+    asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4" : "=&v"(tf) : "v"(t1), "v"(X.y), "v"(Y.y), "v"(Z.y));
+    if constexpr (SLACK) return tn <= tf + 2e-6f * fabsf(tf);
+    else return tn <= tf;
+}
+
 // Slab test on precomputed plane distances (compressed nodes)
 __device__ inline bool box_hit_t(float ax, float bx, float ay, float by, float az, float bz, float t0, float t1,
                                  float& tenter) {
@@ -164,7 +201,6 @@ __device__ inline bool box_hit_t(float ax, float bx, float ay, float by, float a
 // Node box test on the (lo, hi) pair layout: one packed FMA per axis gives both plane distances
 // (v_pk_fma_f32 with the node's SGPR pair, the lane's 1/d and -o/d broadcast by op_sel), the same
 // values as box_hit's six FMAs.
-typedef float pf2 __attribute__((ext_vector_type(2)));
 __device__ inline bool box_hit_pk(const float* cb, f3 oinv, f3 inv, float t0, float t1, float& tenter) {
     const pf2 X = __builtin_elementwise_fma(pf2{cb[0], cb[1]}, pf2{inv.x, inv.x}, pf2{-oinv.x, -oinv.x});
     const pf2 Y = __builtin_elementwise_fma(pf2{cb[2], cb[3]}, pf2{inv.y, inv.y}, pf2{-oinv.y, -oinv.y});
@@ -664,6 +700,8 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
     const float dzs = fabsf(d.z) < 1e-12f ? copysignf(1e-12f, d.z) : d.z;
     const f3 inv = mk3(1.0f / dxs, 1.0f / dys, 1.0f / dzs);
     const f3 oinv = o * inv;
+    // the same constants as VGPR pairs for the packed octant-node plane test (box_hit_pk_nf)
+    [[maybe_unused]] const pf2 ixy = pf2{inv.x, inv.y}, oxy = pf2{oinv.x, oinv.y}, izo = pf2{inv.z, oinv.z};
     // direction signs of the wave's first ray (bit a: negative on axis a): child visiting order
     [[maybe_unused]] const uint32_t rsign = uni((inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u));
     // intersectAABB (gaussianfunctions.glsl:8-16, Q12)
@@ -841,6 +879,13 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
             // (a per-octant min/max-free box test as 8 template copies of the loop measured within noise: +0.7 %;
             // the octant node copies below keep one code path for all octants)
             if (octw) {
+#if GVRT_PK_NF
+#pragma unroll
+                for (int k = 0; k < BVH_W; ++k)
+                    bal[k] = __builtin_amdgcn_ballot_w64(box_hit_pk_nf<SLACK>(
+                        pf2{NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 1)}, pf2{NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 3)},
+                        pf2{NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 5)}, ixy, oxy, izo, tlo, tc));
+#else
                 // (an opaque copy of 1/d: otherwise the first child's plane FMAs, common to both tests, are hoisted
                 // above the branch and every min / max input after it gets a canonicalising v_max)
                 f3 iv = inv;
@@ -850,6 +895,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                     bal[k] = __builtin_amdgcn_ballot_w64(
                         box_hit_nf<SLACK>(NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 1),
                                           NODE_BOX(nd, k, 3), NODE_BOX(nd, k, 5), oinv, iv, tlo, tc));
+#endif
             } else {
 #pragma unroll
             for (int k = 0; k < BVH_W; ++k) {
@@ -1012,7 +1058,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                                     // nothing farther is needed.  The 1e-4 margin keeps the bound
                                     // conservative against ulp differences from the composite's arithmetic.
                                     float Tp = s_T[wid][lane], tt = INF_DIST;
-#pragma unroll
+                        #pragma unroll
                                     for (int i = 0; i < KB; ++i) {
                                         const bool acc_i = kid[i] != INVALID_ID && ka[i] > 0.0f;
                                         Tp = acc_i ? Tp * (1.0f - ka[i]) : Tp;
