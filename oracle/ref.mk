@@ -7,7 +7,7 @@ CXX ?= g++
 INC = -I$(REF)/base -I$(REF)/external -I$(REF)/external/glm -I$(REF)/external/miniply -I$(REF)/external/vulkan
 FLAGS = -O2 -std=c++20 -ffunction-sections -fdata-sections -w
 
-all: _ref/ref_ply_dump _ref/ref_camera_dump
+all: _ref/ref_ply_dump _ref/ref_camera_dump _ref/ref_bench_dump
 
 _ref/%.o: | _ref
 _ref:
@@ -33,3 +33,8 @@ _ref/ref_ply_dump: _ref/ref_ply_dump.o _ref/Vulkan3DGRTModel.o _ref/miniply.o
 CAM_DEFS = -DGLM_FORCE_RADIANS -DGLM_FORCE_DEPTH_ZERO_TO_ONE -DGLM_ENABLE_EXPERIMENTAL
 _ref/ref_camera_dump: ref_camera_dump.cpp $(REF)/base/camera.hpp $(REF)/base/LoadCamera.hpp | _ref
 	$(CXX) -O2 -std=c++17 -ffp-contract=off -w $(CAM_DEFS) -I$(REF)/base -I$(REF)/external/glm -I$(REF)/external/tinygltf $< -o $@
+
+# The reference's vks::Benchmark (base/benchmark.hpp) with its vendored Vulkan headers (types only, nothing
+# linked): writes the reference's fps.txt for given frame times.
+_ref/ref_bench_dump: ref_bench_dump.cpp $(REF)/base/benchmark.hpp | _ref
+	$(CXX) -O2 -std=c++17 -w -I$(REF)/base -I$(REF)/external/vulkan -I$(REF)/external $< -o $@

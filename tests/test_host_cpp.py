@@ -155,3 +155,39 @@ def test_reference_host_interfaces_compile_and_run(gv, tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "splats 300 frames 1 cams 1" in r.stdout and "bench 5 5" in r.stdout
     assert "Benchmark finished" in r.stdout and "device : host-check" in r.stdout
+
+
+REF_BENCH = os.path.join(ROOT, "oracle", "_ref", "ref_bench_dump")
+
+
+@pytest.mark.skipif(not os.path.exists(REF_BENCH), reason="oracle/_ref not built (needs /root/reference)")
+def test_benchmark_fps_txt_matches_reference(tmp_path):
+    """vks::Benchmark::saveResults of the C++ host layer writes the reference's fps.txt byte for byte, and
+    run() / saveResults print the same console lines (base/benchmark.hpp:37-104, built from the reference's
+    sources by oracle/ref.mk): same device line, duration, frame count, fps, per-frame table and
+    best / worst / avg.  Both sides enter the frame times as run()'s loop does."""
+    pkg = os.path.join(ROOT, "3dgvrt_lightfield_amd")
+    exe = str(tmp_path / "bench_results")
+    r = subprocess.run(["g++", "-O1", "-std=c++17", "-ffp-contract=off", "-Wall", "-Werror", "-I", os.path.join(pkg, "host"),
+                        os.path.join(ROOT, "tests", "cpp", "bench_results.cpp"), os.path.join(pkg, "host", "gvrt_host.cpp"),
+                        "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-L", pkg, "-lgvrt", "-L/opt/rocm/lib",
+                        "-lamdhip64", f"-Wl,-rpath,{pkg}", "-Wl,-rpath,/opt/rocm/lib", "-o", exe],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rng = np.random.default_rng(11)
+    cases = [
+        ("AMD Instinct MI355X", "70200", "1", ["1.25", "0.875", "3.0000001"]),
+        ("AMD Instinct MI355X", "70200", "0", ["1.3046", "1.2947"]),
+        ("gfx950 node 7", "4294967295", "1", [repr(float(x)) for x in rng.uniform(0.2, 40.0, 257)]),
+        ("x", "0", "1", ["1e-9", "12345.678901234"]),
+    ]
+    for k, (dev, drv, ft, times) in enumerate(cases):
+        outs = []
+        for prog in (REF_BENCH, exe):
+            f = tmp_path / f"fps_{k}_{os.path.basename(prog)}.txt"
+            p = subprocess.run([prog, str(f), dev, drv, ft, *times], capture_output=True, text=True, timeout=60)
+            assert p.returncode == 0, p.stderr
+            outs.append((f.read_bytes(), p.stdout))
+        assert outs[0][0] == outs[1][0], (outs[0][0][:300], outs[1][0][:300])
+        assert outs[0][1] == outs[1][1], (outs[0][1], outs[1][1])
+        assert outs[0][0].startswith(b"device,driverversion,duration (ms),frames,fps\n" + dev.encode() + b"," + drv.encode())
