@@ -74,6 +74,18 @@ def test_hit_counts_text_layout(tmp_path):
     assert path.read_text() == "0 1 2 \n3 4 5 \n"
 
 
+# SHA-1 of the reference's own printRayHitCounts output (results/texts/rayHitCountsOutput.txt, written by
+# VulkanFullRT.cpp:2182-2195 at 1920x1080).  Every count in that file is 0, so it pins the layout only.
+REF_HIT_COUNTS_SHA1 = "e4b66ece2d1699ddc198bd6c23a8b47a9246821b"
+
+
+def test_hit_counts_text_matches_reference_file(tmp_path):
+    import hashlib
+    path = tmp_path / "rayHitCountsOutput.txt"
+    app.write_hit_counts_txt(str(path), np.zeros((1080, 1920), np.uint32))
+    assert hashlib.sha1(path.read_bytes()).hexdigest() == REF_HIT_COUNTS_SHA1
+
+
 def test_benchmark_csv_layout(tmp_path):
     b = app.Benchmark(warmup=0.0, duration=0.02, filename=str(tmp_path / "fps.txt"), output_frame_times=True)
     b.device, b.driver = "dev", "7.2"
