@@ -576,6 +576,13 @@ __device__ inline uint32_t nz_bit(uint64_t m, uint32_t bit) {
     return r;
 }
 
+#ifndef GVRT_LDS_LANE_FOLD
+#define GVRT_LDS_LANE_FOLD 1
+#endif
+__device__ inline int launder_lane(int l) {
+    asm volatile("" : "+v"(l));
+    return l;
+}
 __device__ inline uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ inline float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
@@ -642,6 +649,14 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
 #endif
     // lane from mbcnt (no register input), wave index uniform
     const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+#if GVRT_LDS_LANE_FOLD
+    // the lane index laundered at each LDS access inside the loops: the loop-invariant per-array addresses
+    // (array base + lane * size) are then not hoisted into VGPRs of their own (one per array, one of which
+    // was spilled to scratch); each access recomputes the shift and folds the base into the DS offset
+#define LL (PACK ? launder_lane(lane) : lane)  // FAST kernels only: LITERAL spilled more with it
+#else
+#define LL lane
+#endif
     const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     // (Round-robin workgroup -> XCD dealing is kept: an XCD-contiguous band remap measured 33 % slower,
     // the bands' very different costs leave a long tail; L2 hit rate is already ~91 %.)
@@ -713,7 +728,13 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
         tminb = fmaxf(0.0f, fmaxf(fminf(t0x, t1x), fmaxf(fminf(t0y, t1y), fminf(t0z, t1z))));
         tmaxb = fminf(fmaxf(t0x, t1x), fminf(fmaxf(t0y, t1y), fmaxf(t0z, t1z)));
     }
-    const float term_cut = a.min_transmittance * 0.9999f;
+    // minTransmittance x 0.9999 (v_mul by the constant, as the compiler forms it), formed where it is used: a
+    // kernel-lifetime copy in a VGPR was spilled to scratch (asm volatile: not hoisted out of the loops)
+    auto term_cut_now = [&]() {
+        float r, k;
+        asm volatile("v_mov_b32 %1, 0x3f7ff972\n\tv_mul_f32 %0, %2, %1" : "=v"(r), "=&v"(k) : "s"(a.min_transmittance));
+        return r;
+    };
     s_last[wid][lane] = fmaxf(0.0f, tminb - EPS_T);
     s_tmax[wid][lane] = tmaxb;
     s_acc[wid][lane] = make_float4(0.0f, 0.0f, 0.0f, a.alpha_init);
@@ -801,8 +822,8 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
         }
         // (GVRT_SOFF: an inactive lane gets tlo = INF_DIST, so no box test of it can hit and the
         // ballots need no AND with the active mask)
-        const float tlo = (!GVRT_SOFF || active) ? s_last[wid][lane] + EPS_T : INF_DIST;
-        const float thi = s_tmax[wid][lane] + EPS_T;
+        const float tlo = (!GVRT_SOFF || active) ? s_last[wid][LL] + EPS_T : INF_DIST;
+        const float thi = s_tmax[wid][LL] + EPS_T;
 #pragma unroll
         for (int i = 0; i < KB; ++i) {
             kt[i] = INF_DIST;
@@ -813,7 +834,8 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
         // drives T below minTransmittance (q sums never exceed the exact depth; +0.5 q of margin)
         uint32_t qneed = 0;
         if constexpr (PACK) {
-            const float Tr = s_T[wid][lane];
+            const float Tr = s_T[wid][LL];
+            const float term_cut = term_cut_now();
             const float need = Tr > term_cut ? __log2f(Tr / term_cut) * QSCALE + 0.5f : 0.0f;
             qneed = (uint32_t)fminf(ceilf(need), 4.0e9f);
         }
@@ -1057,7 +1079,8 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                                     // is the last one that can ever be composited (the loop ends there), so
                                     // nothing farther is needed.  The 1e-4 margin keeps the bound
                                     // conservative against ulp differences from the composite's arithmetic.
-                                    float Tp = s_T[wid][lane], tt = INF_DIST;
+                                    float Tp = s_T[wid][LL], tt = INF_DIST;
+                                    const float term_cut = a.min_transmittance * 0.9999f;
                         #pragma unroll
                                     for (int i = 0; i < KB; ++i) {
                                         const bool acc_i = kid[i] != INVALID_ID && ka[i] > 0.0f;
@@ -1083,9 +1106,9 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
             if (kid[0] == INVALID_ID) {
                 active = false;
             } else {
-                float T = s_T[wid][lane];
-                float4 acc = s_acc[wid][lane];
-                float last = s_last[wid][lane];
+                float T = s_T[wid][LL];
+                float4 acc = s_acc[wid][LL];
+                float last = s_last[wid][LL];
                 // FAST: a buffer that did not fill holds every admitted crossing of (tlo, thi] (nothing was
                 // culled by kt[K-1]; what tcut culled lies past the slot where T drops below
                 // minTransmittance).  Once they are composited nothing is left, so the next round that
@@ -1138,7 +1161,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
 #pragma unroll
                             for (int q = 0; q < GVRT_SH_EARLY / 3; ++q) {
                                 const float4 v0 = shv[3 * q], v1 = shv[3 * q + 1], v2 = shv[3 * q + 2];
-                                const float4 bq = s_basis[wid][q][lane];
+                                const float4 bq = s_basis[wid][q][LL];
                                 er += bq.x * v0.x; eg += bq.x * v0.y; eb += bq.x * v0.z;
                                 er += bq.y * v0.w; eg += bq.y * v1.x; eb += bq.y * v1.y;
                                 er += bq.z * v1.z; eg += bq.z * v1.w; eb += bq.z * v2.x;
@@ -1160,7 +1183,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                             for (int q = 0; q < 4; ++q) {
                                 const float4 v0 = s4[3 * q], v1 = s4[3 * q + 1], v2 = s4[3 * q + 2];
 #endif
-                                const float4 bq = s_basis[wid][q][lane];
+                                const float4 bq = s_basis[wid][q][LL];
                                 const float b0 = bq.x, b1 = bq.y, b2 = bq.z, b3 = bq.w;
                                 // coefficients 4q..4q+3: (v0.xyz) (v0.w v1.xy) (v1.zw v2.x) (v2.yzw)
                                 rr += b0 * v0.x; rg += b0 * v0.y; rb += b0 * v0.z;
@@ -1189,10 +1212,10 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
 #pragma unroll
                     for (int i = KB - CUN; i < KB; ++i) kid[i] = INVALID_ID;
                 }
-                active = full && (last <= s_tmax[wid][lane]) && (T > a.min_transmittance);
-                s_last[wid][lane] = last;
-                s_T[wid][lane] = T;
-                s_acc[wid][lane] = acc;
+                active = full && (last <= s_tmax[wid][LL]) && (T > a.min_transmittance);
+                s_last[wid][LL] = last;
+                s_T[wid][LL] = T;
+                s_acc[wid][LL] = acc;
             }
         }
         if constexpr (STATS) cyc_comp += __builtin_amdgcn_s_memtime() - t_comp0;
