@@ -11,13 +11,31 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("GVRT_LIB_PATH") or os.path.join(_HERE, "libgvrt.so")  # override: A/B builds
+
+
+def _lib_path():
+    """libgvrt.so of this package; GVRT_LIB_PATH may select an A/B variant build, but only one built in-tree
+    under this package (`make variant`, build/<name>/libgvrt.so): any other path is refused."""
+    p = os.environ.get("GVRT_LIB_PATH")
+    if not p:
+        return os.path.join(_HERE, "libgvrt.so")
+    rp = os.path.realpath(p)
+    if not rp.startswith(os.path.realpath(_HERE) + os.sep) or os.path.basename(rp) != "libgvrt.so":
+        raise RuntimeError(f"GVRT_LIB_PATH={p}: only a libgvrt.so built under {_HERE} may be loaded")
+    return rp
+
+
+LIB_PATH = _lib_path()
 
 GVRT_OK = 0
 STATUS_NAMES = {
     0: "GVRT_OK", -1: "GVRT_ERR_INVALID_ARG", -2: "GVRT_ERR_OOM", -3: "GVRT_ERR_HIP",
     -4: "GVRT_ERR_STATE", -5: "GVRT_ERR_NO_DEVICE", -6: "GVRT_ERR_IO", -7: "GVRT_ERR_UNSUPPORTED",
+    -8: "GVRT_ERR_RCCL",
 }
+# per-handle tuning switches (gvrt_set_option; include/gvrt.h GVRT_OPT_*)
+OPTIONS = {"tile_order": 0, "tile_xcd": 1, "octant_nodes": 2, "record_origins": 3, "box_slack": 4,
+           "packed_kbuffer": 5}
 MODE_FAST = 0
 MODE_LITERAL = 1
 
@@ -113,6 +131,8 @@ SIGNATURES = {
     "gvrt_sync": (C.c_int32, [H]),
     "gvrt_set_stream": (C.c_int32, [H, C.c_void_p]),
     "gvrt_set_stats": (C.c_int32, [H, C.c_int]),
+    "gvrt_set_option": (C.c_int32, [H, C.c_uint32, C.c_int64]),
+    "gvrt_get_option": (C.c_int32, [H, C.c_uint32, _P(C.c_int64)]),
     "gvrt_get_device_properties": (C.c_int32, [C.c_int, _P(DeviceProperties)]),
     "gvrt_get_device_buffers": (C.c_int32, [H, _P(DeviceBuffers)]),
     "gvrt_read_accel": (C.c_int32, [H, C.c_int, C.c_void_p, C.c_uint64, _P(C.c_uint64)]),

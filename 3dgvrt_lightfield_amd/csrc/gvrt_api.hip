@@ -323,6 +323,25 @@ gvrt_status gvrt_get_device_buffers(gvrt_handle c, gvrt_device_buffers* out) {
     return GVRT_OK;
 }
 
+gvrt_status gvrt_set_option(gvrt_handle c, uint32_t option, int64_t value) {
+    if (!c) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL handle");
+    if (option >= GVRT_OPT_COUNT) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "unknown option");
+    if (value != 0 && value != 1) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "option values are 0 or 1");
+    if (c->opt[option] == value) return GVRT_OK;
+    GVRT_HIP(c, hipSetDevice(c->device));
+    if (c->async_pending) GVRT_HIP(c, hipStreamSynchronize(c->stream));  // queued launches used the old value
+    c->opt[option] = value;
+    if (option == GVRT_OPT_TILE_ORDER || option == GVRT_OPT_TILE_XCD) c->ord_key = 0;  // the order starts over
+    return GVRT_OK;
+}
+
+gvrt_status gvrt_get_option(gvrt_handle c, uint32_t option, int64_t* value) {
+    if (!c || !value) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL argument");
+    if (option >= GVRT_OPT_COUNT) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "unknown option");
+    *value = c->opt[option];
+    return GVRT_OK;
+}
+
 gvrt_status gvrt_set_stats(gvrt_handle c, int enable) {
     if (!c) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL handle");
     c->stats_on = enable != 0;
@@ -403,14 +422,7 @@ static gvrt_status upload_tile_list(gvrt_context* c, const gvrt_tile* tiles, uin
 // launch records every tile's cost class (log2 of its wave's cycles, 4 classes per octave); one small
 // kernel after it orders the tiles costliest class first, and the next launch of the same frame size
 // dispatches them in that order.  The order changes only which wave renders a tile when, never a pixel.
-// GVRT_TILE_ORDER=0 turns it off.
-static bool tile_order_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("GVRT_TILE_ORDER");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
+// GVRT_OPT_TILE_ORDER = 0 turns it off.
 
 // Arrays of the order for a launch of n tile-list entries: kept while the frame size and the tile list stay
 // the same (list == null: a full frame, whose list is every tile in supertile order), reset otherwise.
@@ -419,7 +431,8 @@ static gvrt_status ensure_tile_order(gvrt_context* c, uint32_t tiles_x, uint32_t
     const uint64_t key = (uint64_t)tiles_x | ((uint64_t)tiles_y << 16) | ((uint64_t)ncams << 32) |
                          (list ? 0ull : (1ull << 63));
     if (c->ord_key == key && c->d_tbucket && (!list || *list == c->ord_list)) return GVRT_OK;
-    GVRT_HIP(c, hipStreamSynchronize(c->stream));  // queued launches may still read the old arrays
+    GVRT_HIP(c, hipStreamSynchronize(c->stream));  // queued launches may still read the old arrays (and
+                                                    // the previous list's upload may still read h_tcode)
     gvrt_dfree(c, (void**)&c->d_tbucket);
     gvrt_dfree(c, (void**)&c->d_thist);
     gvrt_dfree(c, (void**)&c->d_tcode);
@@ -436,7 +449,8 @@ static gvrt_status ensure_tile_order(gvrt_context* c, uint32_t tiles_x, uint32_t
     if (!list) {
         // the full frame as a tile list in the render kernel's supertile order (its first launch's order)
         if ((s = gvrt_dalloc(c, (void**)&c->d_tcode, 4 * n))) return s;
-        std::vector<uint32_t> code;
+        std::vector<uint32_t>& code = c->h_tcode;  // kept: the source of the stream-ordered upload below
+        code.clear();
         code.reserve(n);
         const uint32_t STW = 8, STH = 4;  // as GVRT_ST_W / GVRT_ST_H of gvrt_render.hip
         for (uint32_t cam = 0; cam < ncams; ++cam)
@@ -445,11 +459,11 @@ static gvrt_status ensure_tile_order(gvrt_context* c, uint32_t tiles_x, uint32_t
                     for (uint32_t ty = sy; ty < std::min(sy + STH, tiles_y); ++ty)
                         for (uint32_t tx = sx; tx < std::min(sx + STW, tiles_x); ++tx)
                             code.push_back((cam << 24) | (ty << 12) | tx);
-        GVRT_HIP(c, hipMemcpy(c->d_tcode, code.data(), 4 * n, hipMemcpyHostToDevice));
+        GVRT_HIP(c, hipMemcpyAsync(c->d_tcode, code.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
     } else {
         c->ord_list = *list;
     }
-    GVRT_HIP(c, hipMemset(c->d_thist, 0, 4 * 4 * TILE_BUCKETS));
+    GVRT_HIP(c, hipMemsetAsync(c->d_thist, 0, 4 * 4 * TILE_BUCKETS, c->stream));
     c->ord_parity = 0;
     c->ord_n = n;
     c->ord_key = key;
@@ -493,10 +507,8 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
     for (int k = 0; k < 3; ++k) a.grid_min[k] = c->grid_min[k];
     a.grid_inv = c->grid_inv;
     a.nodes = c->d_nodes4;
-    static const bool oct_off = getenv("GVRT_OCT_NODES") && getenv("GVRT_OCT_NODES")[0] == '0';
-    a.nodes8 = oct_off ? nullptr : c->d_nodes4x8;
+    a.nodes8 = c->opt[GVRT_OPT_OCTANT_NODES] ? c->d_nodes4x8 : nullptr;
     a.nodes8_stride = c->n_nodes4;
-    a.nodes64 = c->d_nodes64;
     a.nrecs = (uint32_t)c->m;
     // the render kernel addresses leaf records (64 B) and 4-wide nodes (128 B) by 32-bit byte offsets
     if (c->n_leaves >= (1ull << 26) || c->n_nodes4 >= (1ull << 25))
@@ -544,8 +556,7 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         float omax = 0.0f;
         for (uint32_t i = 0; i < ncams; ++i)
             for (int k = 12; k < 15; ++k) omax = std::max(omax, std::fabs(view_inverse[16ull * i + k]));
-        static const bool slack_forced = getenv("GVRT_BOX_SLACK") && getenv("GVRT_BOX_SLACK")[0] == '1';
-        a.box_exact = !slack_forced && !c->split_cells && c->box_pad_abs > 0.0f &&
+        a.box_exact = c->opt[GVRT_OPT_BOX_SLACK] == 0 && !c->split_cells && c->box_pad_abs > 0.0f &&
                       std::ldexp(omax, -20) <= c->box_pad_abs;  // also false for a NaN origin
     }
     a.kfast = p->kbuffer_depth ? p->kbuffer_depth : (uint32_t)K_FAST_DEFAULT;
@@ -556,13 +567,18 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         bool one_origin = true;
         for (uint32_t i = 1; i < ncams && one_origin; ++i)
             one_origin = std::memcmp(view_inverse + 16ull * i + 12, view_inverse + 12, 12) == 0;
-        static const bool okrec_off = getenv("GVRT_OKREC") && getenv("GVRT_OKREC")[0] == '0';
         const bool adaptive = (c->enc.opts & 1u) != 0;
-        a.okrec = !okrec_off && one_origin && p->mode == GVRT_MODE_FAST && a.kfast == (uint32_t)K_FAST_DEFAULT &&
-                  !adaptive && a.nrecs < 0xFFFFFFu && !getenv("GVRT_NO_PACK") && c->d_leaf_p && !c->split_cells;
+        a.okrec = c->opt[GVRT_OPT_RECORD_ORIGINS] && one_origin && p->mode == GVRT_MODE_FAST &&
+                  a.kfast == (uint32_t)K_FAST_DEFAULT && !adaptive && a.nrecs < 0xFFFFFFu &&
+                  c->opt[GVRT_OPT_PACKED_KBUFFER] && c->d_leaf_p && !c->split_cells;
         if (a.okrec) {
-            if ((s = gvrt_launch_rec_prep(c, 1, view_inverse + 12))) return s;
-            c->recs_ok = true;
+            // the records already hold this origin's kernel-frame origins when the previous launch had the same
+            // one (a static camera, or the frames of one view): no pass
+            if (!c->recs_ok || std::memcmp(c->rec_origin, view_inverse + 12, 12) != 0) {
+                if ((s = gvrt_launch_rec_prep(c, 1, view_inverse + 12))) return s;
+                std::memcpy(c->rec_origin, view_inverse + 12, 12);
+                c->recs_ok = true;
+            }
         } else if (c->recs_ok) {
             if ((s = gvrt_launch_rec_prep(c, 2, nullptr))) return s;
             c->recs_ok = false;
@@ -580,7 +596,7 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
     }
     // cost-ordered dispatch: full frames and caller tile lists alike (the kernel renders list position
     // perm[i] in workgroup i; outputs stay where the list puts them)
-    const bool ordered = tile_order_enabled() && nwork > 0;
+    const bool ordered = c->opt[GVRT_OPT_TILE_ORDER] != 0 && nwork > 0;
     if (ordered) {
         if ((s = ensure_tile_order(c, tiles_x, tiles_y, ncams, tiles ? &c->h_tiles : nullptr))) return s;
         a.tile_bucket = c->d_tbucket;

@@ -52,10 +52,11 @@ struct gvrt_context {
     gvrt::Bvh4Node* d_nodes4 = nullptr; // 4-wide collapse traversed by the render kernel
     uint64_t n_nodes4 = 0;
     gvrt::Bvh4Node* d_nodes4x8 = nullptr;  // 8 octant copies of d_nodes4 (planes in near / far order)
-    gvrt::Node64* d_nodes64 = nullptr;  // GVRT_NODE64 builds: the compressed copy the render kernel reads
     uint32_t* d_leaf_src = nullptr;  // leaf -> compaction index
     float* d_leaf_p = nullptr;       // leaf positions (3 per leaf): d_recs keeps ok in their place while recs_ok
-    bool recs_ok = false;            // d_recs hold kernel-frame origins for rec_origin (k_rec_origin)
+    // d_recs positions are valid only while !recs_ok: while recs_ok they hold the kernel-frame origins of
+    // rec_origin (k_rec_origin), which every other reader must first restore (gvrt_launch_rec_prep op 2)
+    bool recs_ok = false;
     float rec_origin[3] = {0, 0, 0};
     uint64_t n_leaves = 0;           // BVH leaves: the survivors, or their split pieces
     uint32_t* d_leaf_aux = nullptr;  // split: per leaf {proxy, cell, proxy's cell range lo, hi} (uint4); else null
@@ -101,10 +102,13 @@ struct gvrt_context {
     uint32_t ord_parity = 0;         // parity of the next launch
     uint32_t* d_tcode = nullptr;     // full frames: the tile list (cam << 24 | ty << 12 | tx), supertile order
     uint32_t* d_order = nullptr;     // dispatch order: tile-list positions, costliest class first
+    std::vector<uint32_t> h_tcode;   // host source of d_tcode (kept alive for its stream-ordered upload)
     void* d_stage = nullptr;  // staging for host outputs
     uint64_t stage_cap = 0;
 
     gvrt_stats stats{};
+    // per-handle tuning switches (gvrt_set_option), measured-best defaults
+    int64_t opt[GVRT_OPT_COUNT] = {1, 1, 1, 1, 0, 1};
 };
 
 gvrt_status gvrt_fail(gvrt_context* c, gvrt_status code, const std::string& msg);

@@ -324,79 +324,11 @@ __global__ __launch_bounds__(256) void k_karras(int64_t m, const uint64_t* __res
     if (i == 0) node_parent[0] = -1;
 }
 
-__global__ __launch_bounds__(256) void k_depth(int64_t m, const int32_t* __restrict__ leaf_parent,
-                                               const int32_t* __restrict__ node_parent, uint32_t* out) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= m) return;
-    uint32_t dpt = 1;
-    int32_t p = leaf_parent[j];
-    while (p >= 0 && dpt < 100000) {
-        ++dpt;
-        p = node_parent[p];
-    }
-    atomicMax(out, dpt);
-}
-
-// even-depth flags of binary internal nodes (root depth 0): each becomes one 4-wide node
-__global__ __launch_bounds__(256) void k_even_flags(int64_t ni, const int32_t* __restrict__ node_parent,
-                                                    uint32_t* __restrict__ flags) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > ni) return;
-    if (i == ni) {
-        flags[i] = 0;
-        return;
-    }
-    uint32_t dpt = 0;
-    int32_t p = node_parent[i];
-    while (p >= 0 && dpt < 100000) {
-        ++dpt;
-        p = node_parent[p];
-    }
-    flags[i] = (dpt & 1u) == 0 ? 1u : 0u;
-}
-
 __device__ inline void put_slot(Bvh4Node& o, int k, const float* b, int32_t ref) {
     o.box[k][0] = b[0]; o.box[k][1] = b[3];  // x: lo, hi
     o.box[k][2] = b[1]; o.box[k][3] = b[4];  // y
     o.box[k][4] = b[2]; o.box[k][5] = b[5];  // z
     o.child[k] = ref;
-}
-
-// Collapse: an even-depth node keeps a leaf child as is and replaces an internal child (odd depth)
-// by that child's two children (leaves or even-depth nodes).
-__global__ __launch_bounds__(256) void k_collapse(int64_t ni, const BvhNode* __restrict__ nodes,
-                                                  const uint32_t* __restrict__ flags, const uint32_t* __restrict__ idx4,
-                                                  Bvh4Node* __restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= ni || !flags[i]) return;
-    const BvhNode n = nodes[i];
-    Bvh4Node o;
-    int k = 0;
-    const float* nb = reinterpret_cast<const float*>(&n);
-#pragma unroll
-    for (int side = 0; side < 2; ++side) {
-        const int32_t c = side ? n.c1 : n.c0;
-        if (c < 0) {
-            put_slot(o, k++, nb + 6 * side, c);
-        } else {
-            const BvhNode g = nodes[c];
-            const float* gb = reinterpret_cast<const float*>(&g);
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                const int32_t gc = s2 ? g.c1 : g.c0;
-                put_slot(o, k++, gb + 6 * s2, gc < 0 ? gc : (int32_t)idx4[gc]);
-            }
-        }
-    }
-    const float eb[6] = {EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX, EMPTY_BOX};
-    o.nchild = (uint32_t)k;
-    uint32_t imask = 0;
-    for (int j = 0; j < k; ++j) imask |= o.child[j] >= 0 ? (1u << j) : 0u;
-    for (; k < BVH_W; ++k) put_slot(o, k, eb, 0);
-    o.pad[0] = n.pad0;
-    o.pad[1] = imask;
-    o.pad[2] = 0;
-    out[idx4[i]] = o;
 }
 
 __device__ inline float half_area(const float* b) {
@@ -515,126 +447,11 @@ __global__ __launch_bounds__(256) void k_collapse_level(const BvhNode* __restric
     out[i] = o;
 }
 
-// ---- compressed 64-B nodes (GVRT_NODE64, layout in gvrt_device.h)
-__device__ inline uint16_t h16_bits(_Float16 h) { return __builtin_bit_cast(uint16_t, h); }
-__device__ inline float h16_val(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
-// neighbouring f16 toward -inf / +inf
-__device__ inline uint16_t h16_dn(uint16_t b) {
-    if ((b & 0x7FFFu) == 0) return 0x8001u;  // +-0 -> -smallest subnormal
-    return (b & 0x8000u) ? (uint16_t)(b + 1) : (uint16_t)(b - 1);
-}
-__device__ inline uint16_t h16_up(uint16_t b) {
-    if ((b & 0x7FFFu) == 0) return 0x0001u;
-    return (b & 0x8000u) ? (uint16_t)(b - 1) : (uint16_t)(b + 1);
-}
-// largest f16 <= x, then `extra` further steps down (ok cleared when the result is not finite)
-__device__ inline uint16_t f16_floor(float x, int extra, bool& ok) {
-    uint16_t b = h16_bits((_Float16)x);
-    if (!(h16_val(b) <= x)) b = h16_dn(b);
-    for (int i = 0; i < extra; ++i) b = h16_dn(b);
-    ok = ok && (b & 0x7C00u) != 0x7C00u && x == x;
-    return b;
-}
-__device__ inline uint16_t f16_ceil(float x, int extra, bool& ok) {
-    uint16_t b = h16_bits((_Float16)x);
-    if (!(h16_val(b) >= x)) b = h16_up(b);
-    for (int i = 0; i < extra; ++i) b = h16_up(b);
-    ok = ok && (b & 0x7C00u) != 0x7C00u && x == x;
-    return b;
-}
-
-// leaf children per node (the scan of these gives each node's first leaf slot)
-__global__ __launch_bounds__(256) void k_n64_count(uint64_t n4, const Bvh4Node* __restrict__ in, uint32_t* __restrict__ cnt) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > n4) return;
-    uint32_t c = 0;
-    if (i < n4) {
-        const uint32_t nc = in[i].nchild;
-        for (uint32_t k = 0; k < nc && k < 4; ++k) c += in[i].child[k] < 0 ? 1u : 0u;
-    }
-    cnt[i] = c;
-}
-
-// one compressed node per 4-wide node; perm[leaf slot] = the leaf it holds (leaf order of the build)
-__global__ __launch_bounds__(256) void k_n64_emit(uint64_t n4, const Bvh4Node* __restrict__ in,
-                                                  const uint32_t* __restrict__ off, Node64* __restrict__ out,
-                                                  uint32_t* __restrict__ perm, uint32_t* __restrict__ err) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n4) return;
-    const Bvh4Node n = in[i];
-    const uint32_t nc = n.nchild < 4 ? n.nchild : 4;
-    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (uint32_t k = 0; k < nc; ++k)
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = fminf(lo[a], n.box[k][2 * a]);
-            hi[a] = fmaxf(hi[a], n.box[k][2 * a + 1]);
-        }
-    bool ok = nc > 0;
-    uint16_t ob[3];
-    float org[3];
-    for (int a = 0; a < 3; ++a) {
-        const float ext = nc ? hi[a] - lo[a] : 0.0f;
-        ob[a] = f16_floor(nc ? lo[a] - ext * (1.0f / 1024.0f) : 0.0f, 0, ok);
-        org[a] = h16_val(ob[a]);
-    }
-    Node64 o;
-    uint32_t imask = 0, vmask = 0, ib = 0, ni = 0, nl = 0;
-    for (uint32_t k = 0; k < 4; ++k) {
-        if (k < nc) {
-            vmask |= 1u << k;
-            for (int a = 0; a < 3; ++a) {
-                const uint32_t l16 = f16_floor(n.box[k][2 * a] - org[a], 1, ok);
-                const uint32_t h16 = f16_ceil(n.box[k][2 * a + 1] - org[a], 1, ok);
-                o.box[k][a] = l16 | (h16 << 16);
-            }
-            const int32_t ch = n.child[k];
-            if (ch >= 0) {
-                imask |= 1u << k;
-                if (ni == 0) ib = (uint32_t)ch;
-                else ok = ok && (uint32_t)ch == ib + ni;  // internal children must be contiguous ids
-                ++ni;
-            } else {
-                perm[off[i] + nl] = (uint32_t)~ch;
-                ++nl;
-            }
-        } else {
-            for (int a = 0; a < 3; ++a) o.box[k][a] = 0u;
-        }
-    }
-    const uint32_t meta = imask | (vmask << 4) | ((n.pad[0] & 3u) << 8);
-    o.oxy = (uint32_t)ob[0] | ((uint32_t)ob[1] << 16);
-    o.oz_meta = (uint32_t)ob[2] | (meta << 16);
-    o.inner_base = ib;
-    o.leaf_base = off[i];
-    out[i] = o;
-    if (!ok) atomicOr(err, 1u);
-}
-
-// leaf data into the compressed tree's leaf-slot order
-__global__ __launch_bounds__(256) void k_n64_permute(uint64_t m, const uint32_t* __restrict__ perm,
-                                                     const RenderRec* __restrict__ rin, const float* __restrict__ shin,
-                                                     const uint32_t* __restrict__ srcin, const uint4* __restrict__ auxin,
-                                                     RenderRec* __restrict__ rout, float* __restrict__ shout,
-                                                     uint32_t* __restrict__ srcout, uint4* __restrict__ auxout) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= m) return;
-    const uint32_t t = perm[j];
-    rout[j] = rin[t];
-    if (shin) {
-        const float4* si = reinterpret_cast<const float4*>(shin + 48ull * t);
-        float4* so = reinterpret_cast<float4*>(shout + 48ull * j);
-#pragma unroll
-        for (int k = 0; k < 12; ++k) so[k] = si[k];
-    }
-    srcout[j] = srcin[t];
-    if (auxin) auxout[j] = auxin[t];
-}
-
 }  // namespace
 
 // Surface-area-optimal 4-wide collapse (dynamic programming over the binary tree, after Ylitie, Karras
 // and Laine, "Efficient Incoherent Ray Traversal on GPUs Through Compressed Wide BVHs", HPG 2017 §4),
-// host-side experiment (GVRT_COLLAPSE=dp).  With one proxy per leaf the leaf term of the SAH is the same
+// gvrt_accel_params.collapse = 1 on the host (builders 0, 1, 3).  With one proxy per leaf the leaf term of the SAH is the same
 // for every collapse, so the DP minimises the summed surface area of the 4-wide nodes:
 //   F(leaf, k) = 0;  F(n, 1) = C(n) = SA(n) + min_j F(c0, j) + F(c1, 4 - j);
 //   F(n, k) = min(F(n, k - 1), min_j F(c0, j) + F(c1, k - j))   (k = 2..4)
@@ -644,7 +461,7 @@ static float host_area(const float* b) {
     return ex * ey + ey * ez + ez * ex;
 }
 
-// Binned-SAH binary BVH on the host (builder = 2, GVRT_BUILDER=sah): the trace-quality build of a
+// Binned-SAH binary BVH on the host (builder = 3, the checker of the device build): the trace-quality build of a
 // static scene, the counterpart of the reference's BLAS built once with
 // VK_BUILD_ACCELERATION_STRUCTURE_PREFER_FAST_TRACE_BIT_KHR (VulkanFullRT.cpp:575-787).  Top-down over
 // the Morton-ordered leaf boxes: per range, 32 centroid bins on each axis, the split of least
@@ -680,18 +497,9 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
             return ex * ey + ey * ez + ez * ex;
         }
     };
-    // bins per axis (GVRT_SAH_BINS, default 32) and the range size at or below which the split is an exact
-    // sweep over the sorted centroids instead (GVRT_SAH_EXACT, default 0: binned everywhere)
-    constexpr int NBMAX = 128;
-    static const int NB = [] {
-        const char* e = getenv("GVRT_SAH_BINS");
-        const int v = e ? atoi(e) : 32;
-        return v < 4 ? 4 : (v > NBMAX ? NBMAX : v);
-    }();
-    static const uint32_t EXACT = [] {
-        const char* e = getenv("GVRT_SAH_EXACT");
-        return e ? (uint32_t)atoi(e) : 0u;
-    }();
+    // 32 bins per axis, as the device build (gvrt_sah.hip); 64 / 128 bins or an exact sweep over the sorted
+    // centroids for small ranges measured within noise
+    constexpr int NB = 32, NBMAX = NB;
     // ids by range: the node of [b, e) is id, its left subtree (L leaves) takes ids id + 1 .. id + L - 1
     // and the right child is id + L — independent of the order ranges are processed in, so subtrees
     // build on several threads with the same result
@@ -700,40 +508,6 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
     auto split = [&](const Task& t, Task* kids, int& nk) {
         uint32_t mid = t.b + (t.e - t.b) / 2;
         int axis = 0;
-        const uint32_t n_ = t.e - t.b;
-        if (n_ <= EXACT) {
-            std::vector<uint32_t> ord[3];
-            std::vector<float> ra(n_);
-            float best_cost = INFINITY;
-            int best_axis = -1;
-            uint32_t best_i = 0;
-            for (int a = 0; a < 3; ++a) {
-                ord[a].assign(idx.begin() + t.b, idx.begin() + t.e);
-                std::stable_sort(ord[a].begin(), ord[a].end(),
-                                 [&](uint32_t p, uint32_t q) { return cen[3 * p + a] < cen[3 * q + a]; });
-                Box acc;
-                acc.reset();
-                for (uint32_t i = n_ - 1; i >= 1; --i) {
-                    acc.grow(&bx[6ull * ord[a][i]]);
-                    ra[i] = acc.area();
-                }
-                acc.reset();
-                for (uint32_t i = 1; i < n_; ++i) {
-                    acc.grow(&bx[6ull * ord[a][i - 1]]);
-                    const float cost = acc.area() * (float)i + ra[i] * (float)(n_ - i);
-                    if (cost < best_cost) {
-                        best_cost = cost;
-                        best_axis = a;
-                        best_i = i;
-                    }
-                }
-            }
-            if (best_axis >= 0) {
-                std::copy(ord[best_axis].begin(), ord[best_axis].end(), idx.begin() + t.b);
-                axis = best_axis;
-                mid = t.b + best_i;
-            }
-        } else {
         float cl[3] = {INFINITY, INFINITY, INFINITY}, ch[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (uint32_t i = t.b; i < t.e; ++i)
             for (int a = 0; a < 3; ++a) {
@@ -789,7 +563,6 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
             });
             mid = (uint32_t)(it - idx.begin());
         }  // else every centroid equal: halve the range
-        }
         Box lb, rb;
         lb.reset();
         rb.reset();
@@ -980,79 +753,6 @@ static gvrt_status host_dp_collapse(gvrt_context* c, int32_t root, uint64_t m, s
     return GVRT_OK;
 }
 
-#if GVRT_NODE64
-static_assert(BVH_W == 4, "compressed nodes are 4-wide");
-// Compressed copy of the 4-wide tree for the render kernel, with the leaf data (records, SH, leaf ->
-// compaction index, split aux) moved into leaf-slot order.
-static gvrt_status build_nodes64(gvrt_context* c, uint64_t m) {
-    const uint64_t n4 = c->n_nodes4;
-    uint32_t *cnt = nullptr, *off = nullptr, *perm = nullptr, *err = nullptr, *src2 = nullptr;
-    RenderRec* r2 = nullptr;
-    float* sh2 = nullptr;
-    uint32_t* aux2 = nullptr;
-    void* tmp = nullptr;
-    gvrt_status s = GVRT_OK;
-    auto fin = [&](gvrt_status st) {
-        gvrt_dfree(c, (void**)&cnt);
-        gvrt_dfree(c, (void**)&off);
-        gvrt_dfree(c, (void**)&perm);
-        gvrt_dfree(c, (void**)&err);
-        gvrt_dfree(c, &tmp);
-        gvrt_dfree(c, (void**)&r2);
-        gvrt_dfree(c, (void**)&sh2);
-        gvrt_dfree(c, (void**)&src2);
-        gvrt_dfree(c, (void**)&aux2);
-        return st;
-    };
-#define N64TRY(x)                                \
-    do {                                         \
-        if ((s = (x)) != GVRT_OK) return fin(s); \
-    } while (0)
-#define N64HIP(x, what)                                                \
-    do {                                                               \
-        hipError_t _e = (x);                                           \
-        if (_e != hipSuccess) return fin(gvrt_hip_check(c, _e, what)); \
-    } while (0)
-    gvrt_dfree(c, (void**)&c->d_nodes64);
-    N64TRY(gvrt_dalloc(c, (void**)&c->d_nodes64, sizeof(Node64) * (n4 ? n4 : 1)));
-    N64TRY(gvrt_dalloc(c, (void**)&cnt, 4 * (n4 + 1)));
-    N64TRY(gvrt_dalloc(c, (void**)&off, 4 * (n4 + 1)));
-    N64TRY(gvrt_dalloc(c, (void**)&perm, 4 * m));
-    N64TRY(gvrt_dalloc(c, (void**)&err, 4));
-    N64TRY(gvrt_dalloc(c, (void**)&r2, sizeof(RenderRec) * m));
-    N64TRY(gvrt_dalloc(c, (void**)&src2, 4 * m));
-    if (c->d_sh) N64TRY(gvrt_dalloc(c, (void**)&sh2, 192ull * m));
-    if (c->d_leaf_aux) N64TRY(gvrt_dalloc(c, (void**)&aux2, 16ull * m));
-    size_t tb = 0;
-    N64HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, off, (int)(n4 + 1), c->stream), "scan size");
-    N64TRY(gvrt_dalloc(c, &tmp, tb ? tb : 16));
-    N64HIP(hipMemsetAsync(err, 0, 4, c->stream), "memset");
-    hipLaunchKernelGGL(k_n64_count, dim3((unsigned)((n4 + 1 + 255) / 256)), dim3(256), 0, c->stream, n4, c->d_nodes4, cnt);
-    N64HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, off, (int)(n4 + 1), c->stream), "scan");
-    hipLaunchKernelGGL(k_n64_emit, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, c->stream, n4, c->d_nodes4, off,
-                       c->d_nodes64, perm, err);
-    N64HIP(hipGetLastError(), "k_n64_emit");
-    uint32_t h[2] = {0, 0};
-    N64HIP(hipMemcpyAsync(&h[0], err, 4, hipMemcpyDeviceToHost, c->stream), "err");
-    N64HIP(hipMemcpyAsync(&h[1], off + n4, 4, hipMemcpyDeviceToHost, c->stream), "leaves");
-    N64HIP(hipStreamSynchronize(c->stream), "sync");
-    if (h[0] || h[1] != m)
-        return fin(gvrt_fail(c, GVRT_ERR_UNSUPPORTED,
-                             "compressed nodes: coordinates beyond the f16 range, or a collapse whose internal "
-                             "children are not contiguous"));
-    hipLaunchKernelGGL(k_n64_permute, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, c->stream, m, perm, c->d_recs,
-                       c->d_sh, c->d_leaf_src, reinterpret_cast<const uint4*>(c->d_leaf_aux), r2, sh2, src2,
-                       reinterpret_cast<uint4*>(aux2));
-    N64HIP(hipGetLastError(), "k_n64_permute");
-    std::swap(c->d_recs, r2);
-    std::swap(c->d_leaf_src, src2);
-    if (sh2) std::swap(c->d_sh, sh2);
-    if (aux2) std::swap(c->d_leaf_aux, aux2);
-    return fin(GVRT_OK);  // frees the previous leaf-order buffers
-#undef N64TRY
-#undef N64HIP
-}
-#endif
 
 gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap) {
     const int64_t mp = (int64_t)c->m;  // proxies (survivors)
@@ -1060,7 +760,6 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
     gvrt_dfree(c, (void**)&c->d_sh);
     gvrt_dfree(c, (void**)&c->d_nodes);
     gvrt_dfree(c, (void**)&c->d_nodes4);
-    gvrt_dfree(c, (void**)&c->d_nodes64);
     gvrt_dfree(c, (void**)&c->d_leaf_src);
     gvrt_dfree(c, (void**)&c->d_leaf_aux);
     c->n_nodes4 = 0;
@@ -1255,14 +954,12 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
         c->depth4 = 1;
     } else {
         TRYH(hipMemsetAsync(dep, 0, 4, c->stream), "memset");
-        const char* be = getenv("GVRT_BUILDER");
-        const bool ploc = ap.builder == 1 || (be && be[0] == 'p');  // "ploc": measured 3 % slower to render (more visits), see DESIGN.md
-        // binned SAH: on the device (builder 2, GVRT_BUILDER=sah), or the same algorithm on the host
-        // (builder 3, GVRT_BUILDER=host: the device build's checker, tests/test_gpu_sah.py)
-        const bool sah_host = !ploc && (ap.builder == 3 || (be && be[0] == 'h'));
-        const bool sah_dev = !ploc && !sah_host && (ap.builder == 2 || (be && be[0] == 's'));
-        const char* ce = getenv("GVRT_COLLAPSE");
-        const bool dp = (ap.collapse == 1 || (ce && ce[0] == 'd')) && BVH_W == 4;
+        const bool ploc = ap.builder == 1;  // PLOC: measured 3 % slower to render (more visits), see DESIGN.md
+        // binned SAH: on the device (builder 2), or the same algorithm on the host (builder 3: the device
+        // build's checker, tests/test_gpu_sah.py)
+        const bool sah_host = !ploc && ap.builder == 3;
+        const bool sah_dev = !ploc && !sah_host && ap.builder == 2;
+        const bool dp = ap.collapse == 1;
         std::vector<BvhNode> htree;  // SAH tree kept on the host for the DP collapse
         int32_t root = 0;
         uint32_t sah_depth = 0, sah_d4 = 0;
@@ -1291,8 +988,6 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
                                (const float* const*)dlv);
         }
         const int64_t ni = m - 1;
-        // the even-depth rule needs the Karras layout and 4-wide nodes
-        const bool greedy = ploc || sah_host || sah_dev || BVH_W != 4 || GVRT_NODE64 || !(ce && ce[0] == '0');
         TRYH(hipGetLastError(), "k_karras");
         if (dp && sah_dev) {  // collapsed by gvrt_sah_build_device
             c->depth = sah_depth;
@@ -1305,7 +1000,7 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
             c->depth = d2;
             c->depth4 = d4;
             c->n_nodes4 = n4;
-        } else if (greedy) {
+        } else {
             // ---- greedy surface-area collapse, level by level (upper bound: one 4-wide node per binary node)
             int32_t* src4 = lpar;                                  // lpar (m entries) is free after the hierarchy
             uint32_t* bdep = reinterpret_cast<uint32_t*>(keys);    // the sort keys are free too (8m bytes)
@@ -1346,37 +1041,8 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
             c->depth = hc[1];
             c->depth4 = hc[0] + 1;
             c->n_nodes4 = total;
-        } else {
-        // ---- collapse to the 4-wide tree by even depth (reuse keys/vals as flags / scan)
-        TRYH(hipMemsetAsync(dep, 0, 4, c->stream), "memset");
-        hipLaunchKernelGGL(k_depth, dim3(blocks), dim3(256), 0, c->stream, m, lpar, npar, dep);
-        uint32_t hd = 0;
-        TRYH(hipMemcpyAsync(&hd, dep, 4, hipMemcpyDeviceToHost, c->stream), "depth");
-        uint32_t* flags = reinterpret_cast<uint32_t*>(keys);
-        hipLaunchKernelGGL(k_even_flags, dim3((unsigned)((ni + 1 + 255) / 256)), dim3(256), 0, c->stream, ni, npar,
-                           flags);
-        size_t sb = 0;
-        TRYH(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, flags, vals, (int)(ni + 1), c->stream), "scan size");
-        if (sb > tmp_bytes) {
-            gvrt_dfree(c, &tmp);
-            TRY(gvrt_dalloc(c, &tmp, sb));
-            tmp_bytes = sb;
-        }
-        TRYH(hipcub::DeviceScan::ExclusiveSum(tmp, sb, flags, vals, (int)(ni + 1), c->stream), "scan");
-        uint32_t n4 = 0;
-        TRYH(hipMemcpyAsync(&n4, vals + ni, 4, hipMemcpyDeviceToHost, c->stream), "n4");
-        TRYH(hipStreamSynchronize(c->stream), "sync");
-        c->depth = hd;
-        c->depth4 = (hd + 1) / 2 + 1;
-        hipLaunchKernelGGL(k_collapse, dim3((unsigned)((ni + 255) / 256)), dim3(256), 0, c->stream, ni, c->d_nodes,
-                           flags, vals, c->d_nodes4);
-        TRYH(hipGetLastError(), "k_collapse");
-        c->n_nodes4 = n4;
         }
     }
-#if GVRT_NODE64
-    TRY(build_nodes64(c, (uint64_t)m));
-#endif
     TRYH(hipEventRecord(c->ev1, c->stream), "event");
     TRYH(hipStreamSynchronize(c->stream), "sync");
     float ms = 0.f;

@@ -5,27 +5,29 @@
 // raygenGaussianLightField.rgen:114-202 (multi-camera light field), and the driver's BVH
 // traversal behind traceRayEXT / rayQueryProceedEXT.
 //
-// Mapping to CDNA4: one wave64 = one 8x8 pixel tile (one lane per ray), one wave per workgroup, tiles
-// dispatched in 8x4 supertiles.  Traversal is wave-uniform (packet traversal) over the 4-wide collapse of
-// the LBVH: node and leaf records are addressed by a wave-uniform index and fetched with scalar
-// loads (two s_load_dwordx16 per 128-B node, one per 64-B record), every lane clips its own ray
-// against the four child boxes, and ballots decide which children the packet descends into; the
-// farther children go on a per-wave stack held in two VGPRs (one entry per lane), nearest first by
-// the first hitting lane's entry distance.  Leaves are clipped against the analytic icosahedron (10 antipodal slab pairs in the
-// kernel frame), which yields the same two crossings (entry and exit face, Q1) as the
-// reference's 20-triangle proxy.  Each lane keeps a 16-slot register k-buffer
-// (compareAndSwapHitPayloadValue chain, anyhit.rahit:29-71); a full buffer shrinks that lane's
-// culling distance as the driver's tmax does.  After each traversal round every lane composites
-// its hits front to back (processHit, gaussianfunctions.glsl:153-229) with the SH basis of its
-// ray direction precomputed once per ray (the reference's scalar basis factors, same order).
+// Mapping to CDNA4: one wave64 = one 8x8 pixel tile (one lane per ray), one wave per
+// workgroup, 4 waves per SIMD.  Workgroups take tiles in the order of a tile list: costliest first by the
+// previous launch's per-tile cost classes, each class dealt to the 8 XCDs in contiguous chunks
+// (k_tile_order); the first launch of a frame size walks 8x4-tile supertiles.  Traversal is wave-uniform
+// (packet traversal) over the 4-wide BVH: node and leaf-record addresses are wave-uniform, so both are
+// fetched with scalar loads (two s_load_dwordx16 per 128-B node, one per 64-B record).  A wave whose active
+// rays share one direction octant reads the octant copy of the nodes, whose planes are stored in (near, far)
+// order for that octant.  Every lane clips its own ray against the four child boxes and ballots decide
+// which children the packet descends into; children are visited in the node's stored (split) order,
+// forward or backward by the sign of the first lane's direction on the split axis, and the farther ones go
+// on a 128-entry per-wave LDS stack.  Leaves are tested response first (an accepted crossing passes inside
+// the proxy's inscribed sphere), then clipped against the analytic icosahedron (10 antipodal slab pairs in
+// the kernel frame), which yields the same two crossings (entry and exit face, Q1) as the reference's
+// 20-triangle proxy.  Each lane keeps a register k-buffer (FAST: 24 slots of {t, record id << 8 | q},
+// q a conservative optical-depth code that drives the termination cull; LITERAL: the reference's 16 slots
+// of every crossing, anyhit.rahit:29-71).  After each traversal round every lane composites its slots front
+// to back (processHit, gaussianfunctions.glsl:153-229) with the SH basis of its ray direction precomputed
+// once per ray in LDS.
 //
 // Modes: LITERAL = every crossing enters the k-buffer, rounds exactly as the reference
 // (16 per trace, `last` advanced by rejected hits too).  FAST = only accepted crossings enter the
 // k-buffer; with an exclusive tmin the composited sequence, and therefore the image, is the
-// same (rejected crossings only ever advanced `last`), while far fewer rounds are needed.  FAST
-// also evaluates the response before the clip: an accepted crossing has its line within kS of
-// the centre in the kernel frame, i.e. inside the proxy's inscribed sphere, so a rejected proxy
-// needs no clip at all.
+// same (rejected crossings only ever advanced `last`), while far fewer rounds are needed.
 #include "gvrt_internal.h"
 
 using namespace gvrt;
@@ -41,95 +43,24 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
                 SH_C3_3 = 0.3731763325901154f, SH_C3_4 = -0.4570457994644658f, SH_C3_5 = 1.445305721320277f,
                 SH_C3_6 = -0.5900435899266435f;
 
-// Build switches for A/B experiments (defaults = measured best, same-box A/B in DESIGN.md §4):
-// FMA-form slab test (3 % faster); v_rsq / v_exp in the response (4 % faster, parity unchanged).
-// A software prefetch of the next node / leaf record was measured slower and removed: SMEM returns
-// out of order, so every wait on a record also waited on the prefetch (lgkmcnt(0)).
-#ifndef GVRT_FMA_BOX
-#define GVRT_FMA_BOX 1
-#endif
-#ifndef GVRT_PK_BOX
-#define GVRT_PK_BOX 0  // packed-FMA box test: measured 3 % slower (more VGPRs for the broadcast pairs)
-#endif
-#ifndef GVRT_SH_UNCOND
-#define GVRT_SH_UNCOND 1
-#endif
-#ifndef GVRT_SH_EARLY
-#define GVRT_SH_EARLY 6  // float4 SH loads consumed before the accept branch (multiple of 3, <= 12)
-#endif
-#ifndef GVRT_HM_ASM
-#define GVRT_HM_ASM 1
-#endif
-#ifndef GVRT_SH_PREFETCH
-#define GVRT_SH_PREFETCH 1
-#endif
-// composite: slots per group (static register indices within a group; one buffer shift per group)
-#ifndef GVRT_COMP_UNROLL
-#define GVRT_COMP_UNROLL 6  // FAST K = 24: -1 % vs 4 on bicycle (fewer buffer shifts); 8 spills
-#endif
-#ifndef GVRT_SKIP_EMPTY_ROUND
-#define GVRT_SKIP_EMPTY_ROUND 1
-#endif
-#ifndef GVRT_TCUT
-#define GVRT_TCUT 1
-#endif
-#ifndef GVRT_DIAG_PAIRS
-#define GVRT_DIAG_PAIRS 0
-#endif
-#ifndef GVRT_TCUT_GROUPS
-#define GVRT_TCUT_GROUPS 0
-#endif
-#ifndef GVRT_VSTACK
-#define GVRT_VSTACK 0
-#endif
-// GVRT_TRACE=1 (debug builds only, `make variant V=trace FLAGS=-DGVRT_TRACE=1`): the lane of one chosen
-// pixel records its crossings (kind 1: id, tn, tf, accepted, alpha, round), composites (kind 2: id, t,
-// alpha, T before, accepted, round) and round starts (kind 3: tlo, thi, T, qneed) to a device buffer,
-// read back with gvrt_debug_trace_get (declared only in this build).
-#ifndef GVRT_TRACE
-#define GVRT_TRACE 0
-#endif
-#if GVRT_TRACE
-__device__ float g_trace[8 * 8192];
-__device__ unsigned int g_trace_n;
-__device__ unsigned long long g_trace_pix;
-#define GVRT_TRACE_REC(on, k, x0, x1, x2, x3, x4, x5)                                   \
-    do {                                                                                \
-        if (on) {                                                                       \
-            const unsigned int ti = atomicAdd(&g_trace_n, 1u);                          \
-            if (ti < 8192) {                                                            \
-                float* tr = g_trace + 8 * ti;                                           \
-                tr[0] = (float)(k); tr[1] = (float)(x0); tr[2] = (x1); tr[3] = (x2);     \
-                tr[4] = (x3); tr[5] = (x4); tr[6] = (float)(x5); tr[7] = 0.0f;          \
-            }                                                                           \
-        }                                                                               \
-    } while (0)
-#else
-#define GVRT_TRACE_REC(on, k, x0, x1, x2, x3, x4, x5) do { } while (0)
-#endif
-#ifndef GVRT_APPROX_RESPONSE
-#define GVRT_APPROX_RESPONSE 1
-#endif
-// Slab test, optionally in FMA form t = lo * inv - o * inv (one v_fma per plane).  Culling only: the proxy boxes
-// are padded (1e-5 extent + 1e-6 |centre|, gvrt_enclose.hip) and a relative slack on the exit
-// distance absorbs the rounding, so a crossing is never dropped.
+static_assert(BVH_W == 4, "the render kernel traverses 4-wide nodes");
+
+// Composite tuning (same-box A/B): the first SH_EARLY of a hit's 12 SH float4 loads are
+// consumed before the accept branch, so they are issued with the record's (all 12: spills); the FAST K = 24
+// buffer is composited in groups of COMP_GROUP slots (static register indices, one buffer shift per group).
+constexpr int SH_EARLY = 6;
+constexpr int COMP_GROUP = 6;
+
+// Slab test in FMA form t = lo * inv - o * inv (one v_fma per plane).  Culling only: the proxy boxes are
+// padded (gvrt_enclose.hip), so a crossing is never dropped.
 template <bool SLACK>
-__device__ inline bool box_hit(float lx, float ly, float lz, float hx, float hy, float hz, f3 o, f3 oinv, f3 inv,
-                               float t0, float t1, float& tenter) {
-#if GVRT_FMA_BOX
-    (void)o;
+__device__ inline bool box_hit(float lx, float ly, float lz, float hx, float hy, float hz, f3 oinv, f3 inv,
+                               float t0, float t1) {
     const float ax = fmaf(lx, inv.x, -oinv.x), bx = fmaf(hx, inv.x, -oinv.x);
     const float ay = fmaf(ly, inv.y, -oinv.y), by = fmaf(hy, inv.y, -oinv.y);
     const float az = fmaf(lz, inv.z, -oinv.z), bz = fmaf(hz, inv.z, -oinv.z);
-#else
-    (void)oinv;
-    const float ax = (lx - o.x) * inv.x, bx = (hx - o.x) * inv.x;
-    const float ay = (ly - o.y) * inv.y, by = (hy - o.y) * inv.y;
-    const float az = (lz - o.z) * inv.z, bz = (hz - o.z) * inv.z;
-#endif
     const float tn = fmaxf(fmaxf(t0, fminf(ax, bx)), fmaxf(fminf(ay, by), fminf(az, bz)));
     const float tf = fminf(fminf(t1, fmaxf(ax, bx)), fminf(fmaxf(ay, by), fmaxf(az, bz)));
-    tenter = tn;
     // SLACK: a relative slack on the exit distance absorbs the plane rounding.  Without it the
     // absolute box padding of gvrt_enclose.hip (2^-18 x the scene's position bound) covers the rounding
     // of these FMA-form planes, (2|lo| + 3|o|) * 2^-24 per plane in world units, as long as the ray
@@ -150,83 +81,6 @@ __device__ inline bool box_hit_nf(float nx, float ny, float nz, float fx, float 
     const float tf = fminf(fminf(t1, af), fminf(bf, cf));
     if constexpr (SLACK) return tn <= tf + 2e-6f * fabsf(tf);
     else return tn <= tf;
-}
-
-// Octant-node plane distances by packed FMA: one v_pk_fma_f32 gives an axis's (near, far) pair from the node's
-// SGPR pair, with the lane's 1/d and o/d broadcast to both halves by op_sel / op_sel_hi (negated by neg_lo /
-// neg_hi): the same fma(plane, 1/d, -o/d) values as box_hit_nf's six v_fma_f32, in three instructions.
-// The ray's constants ride in three VGPR pairs: (1/dx, 1/dy), (ox/dx, oy/dy), (1/dz, oz/dz).
-#ifndef GVRT_PK_NF
-#define GVRT_PK_NF 0  // measured within noise to +1 % slower (latency-bound node chain)
-#endif
-typedef float pf2 __attribute__((ext_vector_type(2)));
-__device__ inline pf2 pk_plane_x(pf2 box, pf2 ixy, pf2 oxy) {
-    pf2 r;
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[1,0,0] neg_lo:[0,0,1] neg_hi:[0,0,1]"
-        : "=v"(r) : "s"(box), "v"(ixy), "v"(oxy));
-    return r;
-}
-__device__ inline pf2 pk_plane_y(pf2 box, pf2 ixy, pf2 oxy) {
-    pf2 r;
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,1] op_sel_hi:[1,1,1] neg_lo:[0,0,1] neg_hi:[0,0,1]"
-        : "=v"(r) : "s"(box), "v"(ixy), "v"(oxy));
-    return r;
-}
-__device__ inline pf2 pk_plane_z(pf2 box, pf2 izo) {
-    pf2 r;
-    asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] neg_lo:[0,0,1] neg_hi:[0,0,1]"
-        : "=v"(r) : "s"(box), "v"(izo));
-    return r;
-}
-template <bool SLACK>
-__device__ inline bool box_hit_pk_nf(pf2 bx, pf2 by, pf2 bz, pf2 ixy, pf2 oxy, pf2 izo, float t0, float t1) {
-    const pf2 X = pk_plane_x(bx, ixy, oxy), Y = pk_plane_y(by, ixy, oxy), Z = pk_plane_z(bz, izo);
-    // max / min in asm too: fmaxf / fminf on asm outputs get a canonicalising v_max per input (4 per box)
-    float tn, tf;
-    asm("v_max3_f32 %0, %1, %2, %3\n\tv_max_f32 %0, %0, %4" : "=&v"(tn) : "v"(t0), "v"(X.x), "v"(Y.x), "v"(Z.x));
-    asm("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4" : "=&v"(tf) : "v"(t1), "v"(X.y), "v"(Y.y), "v"(Z.y));
-    if constexpr (SLACK) return tn <= tf + 2e-6f * fabsf(tf);
-    else return tn <= tf;
-}
-
-// Slab test on precomputed plane distances (compressed nodes)
-__device__ inline bool box_hit_t(float ax, float bx, float ay, float by, float az, float bz, float t0, float t1,
-                                 float& tenter) {
-    const float tn = fmaxf(fmaxf(t0, fminf(ax, bx)), fmaxf(fminf(ay, by), fminf(az, bz)));
-    const float tf = fminf(fminf(t1, fmaxf(ax, bx)), fminf(fmaxf(ay, by), fmaxf(az, bz)));
-    tenter = tn;
-    return tn <= tf + 2e-6f * fabsf(tf);
-}
-
-// Node box test on the (lo, hi) pair layout: one packed FMA per axis gives both plane distances
-// (v_pk_fma_f32 with the node's SGPR pair, the lane's 1/d and -o/d broadcast by op_sel), the same
-// values as box_hit's six FMAs.
-__device__ inline bool box_hit_pk(const float* cb, f3 oinv, f3 inv, float t0, float t1, float& tenter) {
-    const pf2 X = __builtin_elementwise_fma(pf2{cb[0], cb[1]}, pf2{inv.x, inv.x}, pf2{-oinv.x, -oinv.x});
-    const pf2 Y = __builtin_elementwise_fma(pf2{cb[2], cb[3]}, pf2{inv.y, inv.y}, pf2{-oinv.y, -oinv.y});
-    const pf2 Z = __builtin_elementwise_fma(pf2{cb[4], cb[5]}, pf2{inv.z, inv.z}, pf2{-oinv.z, -oinv.z});
-    const float tn = fmaxf(fmaxf(t0, fminf(X.x, X.y)), fmaxf(fminf(Y.x, Y.y), fminf(Z.x, Z.y)));
-    const float tf = fminf(fminf(t1, fmaxf(X.x, X.y)), fminf(fmaxf(Y.x, Y.y), fmaxf(Z.x, Z.y)));
-    tenter = tn;
-    return tn <= tf + 2e-6f * fabsf(tf);
-}
-
-template <int K>
-__device__ inline void kb_insert(float t, uint32_t id, float al, float (&kt)[K], uint32_t (&kid)[K], float (&ka)[K]) {
-    if (!(t < kt[K - 1])) return;
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-        const bool sw = t < kt[i];
-        const float tt = kt[i];
-        const uint32_t ti = kid[i];
-        const float ta = ka[i];
-        kt[i] = sw ? t : tt;
-        kid[i] = sw ? id : ti;
-        ka[i] = sw ? al : ta;
-        t = sw ? tt : t;
-        id = sw ? ti : id;
-        al = sw ? ta : al;
-    }
 }
 
 // Insert two crossings of one proxy (a.t <= b.t, either may be INF_DIST) in one pass.  Per slot the
@@ -272,20 +126,14 @@ __device__ inline uint32_t alpha_code(float alpha) {
 }
 
 // As kb_insert2, with one 32-bit payload per slot (t, then payload; same strict-< rule).  The chain
-// runs in groups of G slots, and a group is skipped when no inserting lane has its pending crossing
-// below the group's last slot: the pending pair stays sorted (pt0 <= pt1), so such a group would not
-// change.  With front-to-back traversal most crossings land near the end of the buffer.
-#ifndef GVRT_INSERT_GROUP
-#define GVRT_INSERT_GROUP 8  // 8-slot groups: fewer joins, fewer register copies (4: +4 %, 24: +2 %)
-#endif
-// GVRT_ASM_INSERT: each 8-slot group is one asm block whose slot registers are updated in place ("+v").
-// Left to the compiler, the updated slots of a group landed in fresh registers and the join with the
-// group-skip path copied the whole buffer back (~40 v_mov per executed group for 80 useful VALU).
-// Per slot: 2 v_cmp (to SGPR pairs) + 8 v_cndmask, ordered so that every mask is read at least two
-// instructions after the v_cmp that writes it (the gfx950 VALU-SGPR-write -> lane-mask-read hazard).
-#ifndef GVRT_ASM_INSERT
-#define GVRT_ASM_INSERT 1
-#endif
+// runs in groups of 8 slots (4 when K is not a multiple of 8), and a group is skipped when no inserting
+// lane has its pending crossing below the group's last slot: the pending pair stays sorted (pt0 <= pt1),
+// so such a group would not change.  With front-to-back traversal most crossings land near the end of
+// the buffer.  An 8-slot group is one asm block whose slot registers are updated in place ("+v"): left to
+// the compiler, the updated slots of a group landed in fresh registers and the join with the group-skip
+// path copied the whole buffer back (~40 v_mov per executed group for 80 useful VALU).  Per slot: 2 v_cmp
+// (to SGPR pairs) + 8 v_cndmask, ordered so that every mask is read at least two instructions after the
+// v_cmp that writes it (the gfx950 VALU-SGPR-write -> lane-mask-read hazard).
 #define KB_S_HEAD(T, P)                                      \
     "v_cndmask_b32_e64 %[xt], %[pt0], " T ", %[m0]\n\t"      \
     "v_cmp_lt_f32_e64 %[m1], %[pt1], %[xt]\n\t"              \
@@ -320,21 +168,19 @@ __device__ inline void kb_group8(float& t0, float& t1, float& t2, float& t3, flo
 
 template <int K>
 __device__ inline void kb_insert2p(float ta, float tb, uint32_t pk, float (&kt)[K], uint32_t (&kp)[K]) {
-    constexpr int G = (K % GVRT_INSERT_GROUP == 0) ? GVRT_INSERT_GROUP : 4;
+    constexpr int G = (K % 8 == 0) ? 8 : 4;
     static_assert(K % G == 0, "whole groups");
     float pt0 = ta, pt1 = tb;
     uint32_t pp0 = pk, pp1 = pk;
 #pragma unroll
     for (int g = 0; g < K; g += G) {
         if (__builtin_amdgcn_ballot_w64(pt0 < kt[g + G - 1])) {
-#if GVRT_ASM_INSERT
             if constexpr (G == 8) {
                 kb_group8(kt[g], kt[g + 1], kt[g + 2], kt[g + 3], kt[g + 4], kt[g + 5], kt[g + 6], kt[g + 7], kp[g],
                           kp[g + 1], kp[g + 2], kp[g + 3], kp[g + 4], kp[g + 5], kp[g + 6], kp[g + 7], pt0, pp0, pt1,
                           pp1);
                 continue;
             }
-#endif
 #pragma unroll
             for (int i = g; i < g + G; ++i) {
                 const bool c0 = pt0 < kt[i];
@@ -393,34 +239,21 @@ __device__ inline float len2(f3 v) {
 }
 
 // particleResponse + alpha + the accept test (gaussianfunctions.glsl:192-200); one definition so the
-// insert-time and composite-time evaluations are the same arithmetic
+// insert-time and composite-time evaluations are the same arithmetic (v_rsq / v_exp: parity unchanged)
 __device__ inline bool particle_alpha(f3 ok, f3 dk, float l2, float density, float min_response, float alpha_min,
                                       float& galpha) {
 #pragma clang fp contract(off)
-#if GVRT_APPROX_RESPONSE
     const float rl = l2 > 0.0f ? __builtin_amdgcn_rsqf(l2) : 1.0f;
-#else
-    const float rl = l2 > 0.0f ? 1.0f / sqrtf(l2) : 1.0f;
-#endif
     const float gx = dk.x * rl, gy = dk.y * rl, gz = dk.z * rl;
     const float cx = fmaf(gy, ok.z, -(gz * ok.y));
     const float cy = fmaf(gz, ok.x, -(gx * ok.z));
     const float cz = fmaf(gx, ok.y, -(gy * ok.x));
     const float gd = fmaf(cz, cz, fmaf(cy, cy, cx * cx));
-#if GVRT_APPROX_RESPONSE
     const float gres = __expf((KERNEL_S * gd) * gd);
-#else
-    const float gres = expf((KERNEL_S * gd) * gd);
-#endif
     galpha = fminf(0.99f, gres * density);
     return (gres > min_response) && (galpha > alpha_min);
 }
 
-// Entry / exit distance of a ray through the icosahedron proxy (kernel frame, inradius hk / sqrt(3) *
-// sqrt(3) = kS): the 20 faces lie on 10 antipodal slab pairs |n . x| <= hk with the normals below
-// (particlePrimitives.comp:76-79 vertices; their face planes).  Per slab the crossing interval is
-// centre m = -(n . ok) / (n . dk) +- hk / |n . dk|; the reciprocal is clamped to +-1e30 so a ray
-// parallel to a slab gives an unbounded interval when inside it and an empty one when outside.
 // Cell of the crossing point o + t d (grid of gvrt_lbvh.hip's k_piece_emit), each axis clamped to
 // the proxy's cell range [lo, hi] so that every crossing maps to one of the proxy's pieces; packed 10
 // bits per axis.  Every piece of a proxy evaluates the same expression on the same record, so a
@@ -437,6 +270,11 @@ __device__ inline uint32_t crossing_cell(f3 o, f3 d, float t, const RenderArgs& 
     return c;
 }
 
+// Entry / exit distance of a ray through the icosahedron proxy (kernel frame, inradius hk / sqrt(3) *
+// sqrt(3) = kS): the 20 faces lie on 10 antipodal slab pairs |n . x| <= hk with the normals below
+// (particlePrimitives.comp:76-79 vertices; their face planes).  Per slab the crossing interval is
+// centre m = -(n . ok) / (n . dk) +- hk / |n . dk|; the reciprocal is clamped to +-1e30 so a ray
+// parallel to a slab gives an unbounded interval when inside it and an empty one when outside.
 __device__ inline void ico_clip(f3 ok, f3 dk, float hk, float& tn, float& tf) {
     float lo = -INFINITY, hi = INFINITY;
     // one slab at a time (short live ranges: this runs with the whole k-buffer in registers)
@@ -475,52 +313,25 @@ __device__ inline void ico_clip(f3 ok, f3 dk, float hk, float& tn, float& tf) {
     tf = hi;
 }
 
-__device__ inline int32_t writelane(int32_t old, int32_t v, int32_t lane) {
-    // gfx9 constant-bus rule: with an SGPR source the lane select must come from M0
-    asm("v_writelane_b32 %0, %1, m0" : "+v"(old) : "s"(v), "{m0}"(lane));  // not volatile: no memory effects
-    return old;
-}
-
-// arr[k] for a wave-uniform k: a select chain (s_cmp / s_cselect) over the register array.  A macro,
-// not a function taking the array by reference: that form pushed the arrays to scratch (+55 % time).
-#if GVRT_BVH_W == 4
+// arr[k] for a wave-uniform k: a select chain (s_cmp / s_cselect) over the four values.  A macro, not a
+// function taking the array by reference: that form pushed the arrays to scratch (+55 % time).
 template <typename T>
 __device__ inline T sel4(T a0, T a1, T a2, T a3, uint32_t k) {  // values, not an array: stays s_cselect
     const T lo = (k & 1u) ? a1 : a0, hi = (k & 1u) ? a3 : a2;
     return (k & 2u) ? hi : lo;
 }
 #define GVRT_PICK(a, k) sel4((a)[0], (a)[1], (a)[2], (a)[3], (uint32_t)(k))
-#else
-#define GVRT_PICK(a, k)                                                                                  \
-    ((k) == 0 ? (a)[0] : (k) == 1 ? (a)[1] : (k) == 2 ? (a)[2] : (k) == 3 ? (a)[3] : (k) == 4 ? (a)[4] \
-     : (k) == 5 ? (a)[5] : (k) == 6 ? (a)[6] : (a)[7])
-#endif
 
-// Node fetch.  The compiler splits a 128-B node into dwordx16 + dwordx8 + dwordx4 + dword loads with
-// lgkmcnt waits between them (three dependent scalar round trips per node visit); GVRT_ASM_NODE issues
-// the two s_load_dwordx16 back to back and waits once.
-#ifndef GVRT_ASM_NODE
-#define GVRT_ASM_NODE 1
-#endif
-#ifndef GVRT_SOFF
-#define GVRT_SOFF 1  // SGPR-offset node / record loads, inactive lanes excluded through tlo (no mask ANDs)
-#endif
-#if GVRT_ASM_NODE && GVRT_BVH_W == 4
+// Node fetch.  The compiler split a 128-B node into dwordx16 + dwordx8 + dwordx4 + dword loads with
+// lgkmcnt waits between them (three dependent scalar round trips per node visit); the asm issues the two
+// s_load_dwordx16 back to back and waits once.  The node's 32-bit byte offset rides in the loads' SGPR
+// offset field (one shift instead of 64-bit pointer arithmetic per visit); so does a record's.
 typedef int32_t sv16 __attribute__((ext_vector_type(16)));
 struct NodeS {
     sv16 a, b;  // dwords 0..15, 16..31 of a Bvh4Node
     __device__ int32_t w(int i) const { return i < 16 ? a[i] : b[i - 16]; }
     __device__ float f(int i) const { return __int_as_float(w(i)); }
 };
-__device__ inline NodeS load_node(const Bvh4Node* __restrict__ p) {
-    NodeS n;
-    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&s"(n.a), "=&s"(n.b)
-                 : "s"(p));
-    return n;
-}
-// node `idx` of the array at `base`: the 32-bit byte offset rides in the loads' SGPR offset field
-// (one shift instead of 64-bit pointer arithmetic per visit)
 __device__ inline NodeS load_node_at(const Bvh4Node* __restrict__ base, int32_t idx) {
     NodeS n;
     const uint32_t off = (uint32_t)idx << 7;
@@ -535,30 +346,9 @@ __device__ inline RenderRec load_rec_at(const RenderRec* __restrict__ base, int3
     asm volatile("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
     return __builtin_bit_cast(RenderRec, v);
 }
-#if GVRT_NODE64
-// compressed node `idx` (64 B): one s_load_dwordx16
-__device__ inline sv16 load_node64_at(const Node64* __restrict__ base, int32_t idx) {
-    sv16 v;
-    const uint32_t off = (uint32_t)idx << 6;
-    asm volatile("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
-    return v;
-}
-// f16 halves of a node dword as f32 (the conversion folds into v_fma_mix_f32's op_sel)
-__device__ inline float h16lo(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(w & 0xFFFFu)); }
-__device__ inline float h16hi(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16)); }
-#endif
 #define NODE_BOX(nd, k, j) (nd).f(6 * (k) + (j))
 #define NODE_CHILD(nd, k) (nd).w(24 + (k))
 #define NODE_PAD(nd, j) (nd).w(29 + (j))
-#else
-#undef GVRT_SOFF
-#define GVRT_SOFF 0
-typedef Bvh4Node NodeS;
-__device__ inline NodeS load_node(const Bvh4Node* __restrict__ p) { return *p; }
-#define NODE_BOX(nd, k, j) (nd).box[k][j]
-#define NODE_CHILD(nd, k) (nd).child[k]
-#define NODE_PAD(nd, j) (nd).pad[j]
-#endif
 
 // lane id recomputed at the point of use (asm volatile: not merged with the kernel-entry value, so no
 // register holds it through the traversal)
@@ -576,92 +366,54 @@ __device__ inline uint32_t nz_bit(uint64_t m, uint32_t bit) {
     return r;
 }
 
-#ifndef GVRT_LDS_LANE_FOLD
-#define GVRT_LDS_LANE_FOLD 1
-#endif
+// The lane index laundered at each LDS access inside the loops (FAST kernels): the loop-invariant per-array
+// addresses (array base + lane * size) are then not hoisted into VGPRs of their own (one per array, one of
+// which was spilled to scratch); each access recomputes the shift and folds the base into the DS offset.
 __device__ inline int launder_lane(int l) {
     asm volatile("" : "+v"(l));
     return l;
 }
 __device__ inline uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ inline float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 
-// Waves per SIMD the register allocator must fit: 4 (<= 128 VGPRs) measured fastest, ahead of 3 (no
-// spills) and 5 (heavy spills); see DESIGN.md §4.
-// Workgroup shape: GVRT_WG_WAVES waves (8x8 tiles) per workgroup, laid out GVRT_WG_TW tiles wide.
-// One wave per workgroup: a finished wave's slot and LDS go to the next tile at once instead of waiting for
-// the slowest wave of its workgroup (tiles of one block differ in cost): 5.5 % / 4.4 % / 3.2 % faster than
-// 2 x 2 tiles on bicycle / dense / garden; 2 x 1 within noise of it, 1 x 2 between.
-#ifndef GVRT_WG_WAVES
-#define GVRT_WG_WAVES 1
-#endif
-#ifndef GVRT_WG_TW
-#define GVRT_WG_TW 1
-#endif
-// Dispatch order: workgroups walk 8 x 4-block supertiles (64 x 32 px with one-wave workgroups) in row-major
-// order, so the tiles in flight form a compact band: 0.9 / 2.0 / 1.8 % faster than row-major on bicycle /
-// dense / garden (4 x 4: mixed, 16 x 8: within noise).
-#ifndef GVRT_EXP_TILECOST
-#define GVRT_EXP_TILECOST 0
-#endif
-#ifndef GVRT_ST_W
-#define GVRT_ST_W 8
-#endif
-#ifndef GVRT_ST_H
-#define GVRT_ST_H 4
-#endif
-constexpr int WGW = GVRT_WG_WAVES, WG_TW = GVRT_WG_TW, WG_TH = GVRT_WG_WAVES / GVRT_WG_TW;
-constexpr uint32_t ST_W = GVRT_ST_W, ST_H = GVRT_ST_H;  // supertile of workgroup blocks (dispatch order)
-static_assert(WG_TW * WG_TH == WGW, "workgroup tile block");
-
-#ifndef GVRT_RENDER_MIN_WAVES
-#define GVRT_RENDER_MIN_WAVES 4
-#endif
-
-#if GVRT_NODE64
-typedef Node64 NodeT;
-#else
-typedef Bvh4Node NodeT;
-#endif
+// Dispatch geometry.  One wave per workgroup: a finished wave's slot and LDS go to the next tile at once
+// (5.5 % / 4.4 % / 3.2 % faster than 2 x 2-tile workgroups on bicycle / dense / garden).  Without a tile
+// list, workgroups walk ST_W x ST_H supertiles of tiles in row-major order (0.9 / 2.0 / 1.8 % faster than
+// row-major tiles).  4 waves per SIMD (<= 128 VGPRs) measured fastest, ahead of 3 (no spills) and 5 (heavy
+// spills or a smaller k-buffer).
+constexpr uint32_t ST_W = 8, ST_H = 4;
+constexpr int RENDER_MIN_WAVES = 4;
 
 template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK, bool SLACK, bool OKREC>
-__global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_render(const RenderArgs a, const NodeT* __restrict__ nodes_,
-                                                const RenderRec* __restrict__ recs_, const RenderRec* __restrict__ crecs_,
-                                                const uint4* __restrict__ aux_, const float* __restrict__ sh_,
-                                                const float* __restrict__ view_inv_, const uint32_t* __restrict__ tiles_,
-                                                uint8_t* __restrict__ rgba8_, float* __restrict__ rgba32f_,
-                                                float* __restrict__ ray_dirs_, uint32_t* __restrict__ hit_counts_,
-                                                unsigned long long* __restrict__ stats_) {
+__global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArgs a, const Bvh4Node* __restrict__ nodes_,
+                                                                 const RenderRec* __restrict__ recs_,
+                                                                 const RenderRec* __restrict__ crecs_,
+                                                                 const uint4* __restrict__ aux_,
+                                                                 const float* __restrict__ sh_,
+                                                                 const float* __restrict__ view_inv_,
+                                                                 const uint32_t* __restrict__ tiles_,
+                                                                 uint8_t* __restrict__ rgba8_,
+                                                                 float* __restrict__ rgba32f_,
+                                                                 float* __restrict__ ray_dirs_,
+                                                                 uint32_t* __restrict__ hit_counts_,
+                                                                 unsigned long long* __restrict__ stats_) {
     // SH basis of each lane's ray direction, chunk-major so one ds_read_b128 per chunk is
     // conflict-free (16 KB per block; occupancy is VGPR-bound, not LDS-bound)
-    __shared__ float4 s_basis[WGW][4][64];
+    __shared__ float4 s_basis[4][64];
     // composite state (rgb, alpha accumulator) and transmittance, parked in LDS during traversal so
     // their VGPRs go to the k-buffer (2 x KB registers)
-    __shared__ float4 s_acc[WGW][64];
-    __shared__ float s_T[WGW][64];
-    __shared__ float s_last[WGW][64];  // `last` and the AABB exit: round-boundary state, not needed in traversal
-    __shared__ float s_tmax[WGW][64];
-    __shared__ uint32_t s_pxy[WGW][64];  // px | py << 16, parked for the output stage (not live in VGPRs)
-    __shared__ unsigned long long s_t0[WGW];  // wave start (s_memtime), for the per-tile cost class
-#if !GVRT_VSTACK
-    __shared__ int32_t s_stack[WGW][STACK_DEPTH];
-#endif
-    // lane from mbcnt (no register input), wave index uniform
+    __shared__ float4 s_acc[64];
+    __shared__ float s_T[64];
+    __shared__ float s_last[64];  // `last` and the AABB exit: round-boundary state, not needed in traversal
+    __shared__ float s_tmax[64];
+    __shared__ uint32_t s_pxy[64];  // px | py << 16, parked for the output stage (not live in VGPRs)
+    __shared__ unsigned long long s_t0;  // wave start (s_memtime), for the per-tile cost class
+    __shared__ int32_t s_stack[STACK_DEPTH];
+    // lane from mbcnt (no register input)
     const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-#if GVRT_LDS_LANE_FOLD
-    // the lane index laundered at each LDS access inside the loops: the loop-invariant per-array addresses
-    // (array base + lane * size) are then not hoisted into VGPRs of their own (one per array, one of which
-    // was spilled to scratch); each access recomputes the shift and folds the base into the DS offset
 #define LL (PACK ? launder_lane(lane) : lane)  // FAST kernels only: LITERAL spilled more with it
-#else
-#define LL lane
-#endif
-    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    // (Round-robin workgroup -> XCD dealing is kept: an XCD-contiguous band remap measured 33 % slower,
-    // the bands' very different costs leave a long tail; L2 hit rate is already ~91 %.)
     // tile-list position: the cost-ordered permutation of the list, or the workgroup's own
-    const uint64_t tile_idx = a.perm ? (uint64_t)a.perm[blockIdx.x] : (uint64_t)blockIdx.x * WGW + wid;
+    const uint64_t tile_idx = a.perm ? (uint64_t)a.perm[blockIdx.x] : (uint64_t)blockIdx.x;
     uint32_t cam, tx, ty;
     if (tiles_) {
         if (tile_idx >= a.ntiles) return;  // wave-uniform
@@ -670,29 +422,20 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
         ty = (t >> 12) & 0xFFFu;
         tx = t & 0xFFFu;
     } else {
-        // workgroup = a WG_TW x WG_TH block of tiles; blocks in row-major order of ST_W x ST_H supertiles
-        // (row-major inside), per camera
-        const uint32_t bx_n = (a.tiles_x + WG_TW - 1) / WG_TW, by_n = (a.tiles_y + WG_TH - 1) / WG_TH;
-        const uint32_t sx_n = (bx_n + ST_W - 1) / ST_W, sy_n = (by_n + ST_H - 1) / ST_H;
+        // tiles in row-major order of ST_W x ST_H supertiles (row-major inside), per camera
+        const uint32_t sx_n = (a.tiles_x + ST_W - 1) / ST_W, sy_n = (a.tiles_y + ST_H - 1) / ST_H;
         const uint64_t per = (uint64_t)sx_n * sy_n * (ST_W * ST_H);
         const uint64_t bid = blockIdx.x;
         cam = (uint32_t)(bid / per);
         const uint32_t rem = (uint32_t)(bid % per);
         const uint32_t st = rem / (ST_W * ST_H), in = rem % (ST_W * ST_H);
-        const uint32_t by = (st / sx_n) * ST_H + in / ST_W, bx = (st % sx_n) * ST_W + in % ST_W;
-        ty = by * WG_TH + (uint32_t)wid / WG_TW;
-        tx = bx * WG_TW + (uint32_t)wid % WG_TW;
+        ty = (st / sx_n) * ST_H + in / ST_W;
+        tx = (st % sx_n) * ST_W + in % ST_W;
         if (tx >= a.tiles_x || ty >= a.tiles_y) return;  // wave-uniform: tile outside the frame
     }
     cam = uni(cam);
     const uint32_t px = tx * 8 + (lane & 7), py = ty * 8 + (lane >> 3);
     const bool valid = px < a.width && py < a.height && cam < a.ncams;
-#if GVRT_EXP_TILECOST  // timing probe: the hit-count output receives the wave's cycles
-    const uint64_t exp_t0 = __builtin_amdgcn_s_memtime();
-#endif
-#if GVRT_TRACE
-    const bool trace_on = valid && ((uint64_t)cam * a.height + py) * a.width + px == g_trace_pix;
-#endif
 
     // ---- ray generation (particleRendering.comp:123-129, raygen.rgen:116-121)
     const float* V = view_inv_ + 16 * (cam < a.ncams ? cam : 0);
@@ -715,10 +458,8 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
     const float dzs = fabsf(d.z) < 1e-12f ? copysignf(1e-12f, d.z) : d.z;
     const f3 inv = mk3(1.0f / dxs, 1.0f / dys, 1.0f / dzs);
     const f3 oinv = o * inv;
-    // the same constants as VGPR pairs for the packed octant-node plane test (box_hit_pk_nf)
-    [[maybe_unused]] const pf2 ixy = pf2{inv.x, inv.y}, oxy = pf2{oinv.x, oinv.y}, izo = pf2{inv.z, oinv.z};
     // direction signs of the wave's first ray (bit a: negative on axis a): child visiting order
-    [[maybe_unused]] const uint32_t rsign = uni((inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u));
+    const uint32_t rsign = uni((inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u));
     // intersectAABB (gaussianfunctions.glsl:8-16, Q12)
     float tminb, tmaxb;
     {
@@ -735,12 +476,12 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
         asm volatile("v_mov_b32 %1, 0x3f7ff972\n\tv_mul_f32 %0, %2, %1" : "=v"(r), "=&v"(k) : "s"(a.min_transmittance));
         return r;
     };
-    s_last[wid][lane] = fmaxf(0.0f, tminb - EPS_T);
-    s_tmax[wid][lane] = tmaxb;
-    s_acc[wid][lane] = make_float4(0.0f, 0.0f, 0.0f, a.alpha_init);
-    s_T[wid][lane] = 1.0f;
-    s_pxy[wid][lane] = px | py << 16;
-    if (a.tile_bucket) s_t0[wid] = __builtin_amdgcn_s_memtime();
+    s_last[lane] = fmaxf(0.0f, tminb - EPS_T);
+    s_tmax[lane] = tmaxb;
+    s_acc[lane] = make_float4(0.0f, 0.0f, 0.0f, a.alpha_init);
+    s_T[lane] = 1.0f;
+    s_pxy[lane] = px | py << 16;
+    if (a.tile_bucket) s_t0 = __builtin_amdgcn_s_memtime();
     // counters: only the STATS instantiation keeps them (registers); the accepted-hit count is
     // recovered exactly from the alpha accumulator (RQ/RT alpha = alpha_init + #accepted, Q10)
     uint32_t nproc = 0, rounds = 0;
@@ -751,7 +492,6 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
     uint32_t w_rounds = 0, w_late = 0;  // traversal rounds of this wave; node visits after the first round
     [[maybe_unused]] const uint64_t cyc_start = STATS ? __builtin_amdgcn_s_memtime() : 0;
     bool active = valid && a.nrecs > 0 && (fmaxf(0.0f, tminb - EPS_T) <= tmaxb) && (1.0f > a.min_transmittance);
-#if !GVRT_NODE64
     // a wave whose active rays share one direction octant reads that octant's node copy (planes in near / far
     // order, box_hit_nf); waves straddling an axis sign (a few tiles on the lines where a direction component
     // changes sign) read the plain nodes
@@ -764,53 +504,35 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
         octw = __builtin_amdgcn_ballot_w64(active && oct != oct0) == 0;
         if (octw) nbase = a.nodes8 + a.nodes8_stride * oct0;
     }
-#endif
 
     static_assert(!(LITERAL && PACK), "LITERAL keeps rejected crossings: unpacked k-buffer");
     float kt[KB];
     uint32_t kid[KB];       // record id, or the packed payload (id << 8 | q) when PACK
     float ka[PACK ? 1 : KB];  // alpha per slot (unpacked only; < 0 = rejected crossing in LITERAL)
-#if GVRT_VSTACK
-    // Per-wave traversal stack in two VGPRs, entry i in lane i & 63 of stk[i >> 6] (v_writelane /
-    // v_readlane with a uniform index: no LDS round trip on a pop)
-    static_assert(STACK_DEPTH == 128, "two VGPRs of 64 lanes");
-    int32_t stk0 = 0, stk1 = 0;
-    int sp = 0;
-    auto push = [&](int32_t v) {
-        if (sp < 64) stk0 = writelane(stk0, v, sp);
-        else stk1 = writelane(stk1, v, sp - 64);
-        ++sp;
-    };
-    auto pop = [&]() -> int32_t {
-        --sp;
-        return sp < 64 ? __builtin_amdgcn_readlane(stk0, sp) : __builtin_amdgcn_readlane(stk1, sp - 64);
-    };
-#else
     // Per-wave traversal stack in LDS
-    int32_t* stack = s_stack[wid];
+    int32_t* stack = s_stack;
     int sp = 0;
     auto push = [&](int32_t v) { stack[sp++] = v; };
     auto pop = [&]() -> int32_t { return unii(stack[--sp]); };
-#endif
     {
         // radianceFromSpH basis factors (gaussianfunctions.glsl:122-151), signs folded, zero past
         // sph_eval_degree; computed once per ray and kept in LDS (not registers) through the traversal
         const float x = d.x, y = d.y, z = d.z;
         const uint32_t deg = a.sph_deg;
         const float xx = x * x, yy = y * y, zz = z * z;
-        s_basis[wid][0][lane] = make_float4(SH_C0, deg > 0 ? -(SH_C1 * y) : 0.f, deg > 0 ? SH_C1 * z : 0.f,
-                                            deg > 0 ? -(SH_C1 * x) : 0.f);
-        s_basis[wid][1][lane] = make_float4(deg > 1 ? SH_C2_0 * (x * y) : 0.f, deg > 1 ? SH_C2_1 * (y * z) : 0.f,
-                                            deg > 1 ? SH_C2_2 * (2.0f * zz - xx - yy) : 0.f,
-                                            deg > 1 ? SH_C2_3 * (x * z) : 0.f);
-        s_basis[wid][2][lane] = make_float4(deg > 1 ? SH_C2_4 * (xx - yy) : 0.f,
-                                            deg > 2 ? SH_C3_0 * y * (3.0f * xx - yy) : 0.f,
-                                            deg > 2 ? SH_C3_1 * (x * y) * z : 0.f,
-                                            deg > 2 ? SH_C3_2 * y * (4.0f * zz - xx - yy) : 0.f);
-        s_basis[wid][3][lane] = make_float4(deg > 2 ? SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) : 0.f,
-                                            deg > 2 ? SH_C3_4 * x * (4.0f * zz - xx - yy) : 0.f,
-                                            deg > 2 ? SH_C3_5 * z * (xx - yy) : 0.f,
-                                            deg > 2 ? SH_C3_6 * x * (xx - 3.0f * yy) : 0.f);
+        s_basis[0][lane] = make_float4(SH_C0, deg > 0 ? -(SH_C1 * y) : 0.f, deg > 0 ? SH_C1 * z : 0.f,
+                                       deg > 0 ? -(SH_C1 * x) : 0.f);
+        s_basis[1][lane] = make_float4(deg > 1 ? SH_C2_0 * (x * y) : 0.f, deg > 1 ? SH_C2_1 * (y * z) : 0.f,
+                                       deg > 1 ? SH_C2_2 * (2.0f * zz - xx - yy) : 0.f,
+                                       deg > 1 ? SH_C2_3 * (x * z) : 0.f);
+        s_basis[2][lane] = make_float4(deg > 1 ? SH_C2_4 * (xx - yy) : 0.f,
+                                       deg > 2 ? SH_C3_0 * y * (3.0f * xx - yy) : 0.f,
+                                       deg > 2 ? SH_C3_1 * (x * y) * z : 0.f,
+                                       deg > 2 ? SH_C3_2 * y * (4.0f * zz - xx - yy) : 0.f);
+        s_basis[3][lane] = make_float4(deg > 2 ? SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) : 0.f,
+                                       deg > 2 ? SH_C3_4 * x * (4.0f * zz - xx - yy) : 0.f,
+                                       deg > 2 ? SH_C3_5 * z * (xx - yy) : 0.f,
+                                       deg > 2 ? SH_C3_6 * x * (xx - 3.0f * yy) : 0.f);
     }
 
     while (__ballot(active)) {
@@ -820,10 +542,10 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
         if constexpr (LITERAL || STATS) {
             if (active) ++rounds;
         }
-        // (GVRT_SOFF: an inactive lane gets tlo = INF_DIST, so no box test of it can hit and the
-        // ballots need no AND with the active mask)
-        const float tlo = (!GVRT_SOFF || active) ? s_last[wid][LL] + EPS_T : INF_DIST;
-        const float thi = s_tmax[wid][LL] + EPS_T;
+        // (an inactive lane gets tlo = INF_DIST, so no box test of it can hit and the ballots need no AND with
+        // the active mask)
+        const float tlo = active ? s_last[LL] + EPS_T : INF_DIST;
+        const float thi = s_tmax[LL] + EPS_T;
 #pragma unroll
         for (int i = 0; i < KB; ++i) {
             kt[i] = INF_DIST;
@@ -834,17 +556,15 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
         // drives T below minTransmittance (q sums never exceed the exact depth; +0.5 q of margin)
         uint32_t qneed = 0;
         if constexpr (PACK) {
-            const float Tr = s_T[wid][LL];
+            const float Tr = s_T[LL];
             const float term_cut = term_cut_now();
             const float need = Tr > term_cut ? __log2f(Tr / term_cut) * QSCALE + 0.5f : 0.0f;
             qneed = (uint32_t)fminf(ceilf(need), 4.0e9f);
         }
         uint32_t qtot = 0;  // PACK: sum of the q codes inserted this round (>= the buffer's sum)
-        GVRT_TRACE_REC(trace_on && active, 3, 0, tlo, thi, s_T[wid][lane], (float)qneed, rounds);
 
-        // ---------------- trace(): packet traversal of the 4-wide LBVH
+        // ---------------- trace(): packet traversal of the 4-wide BVH
         float tcut = INF_DIST;  // termination-aware cull distance of this lane (see the leaf insert)
-        [[maybe_unused]] const uint64_t amask = __builtin_amdgcn_ballot_w64(active);
         sp = 0;
         int32_t cur = 0;  // node index (wave-uniform); the node is fetched at the top of each visit so its
                           // 32 SGPRs are not loop-carried
@@ -853,61 +573,13 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
             [[maybe_unused]] uint64_t t_node0 = 0;
             if constexpr (STATS) {
                 ++w_nodes;
-                if constexpr (!GVRT_DIAG_PAIRS) w_late += w_rounds > 1 ? 1u : 0u;
+                w_late += w_rounds > 1 ? 1u : 0u;
                 t_node0 = __builtin_amdgcn_s_memtime();  // the node phase includes the fetch
             }
-#if GVRT_NODE64
-            const sv16 nd = load_node64_at(nodes_, unii(cur));  // whole node: one s_load_dwordx16
-#elif GVRT_SOFF
-            const NodeS nd = load_node_at(nbase, unii(cur));  // whole node: 2x s_load_dwordx16 (4-wide)
-#else
-            const NodeS nd = load_node(nodes_ + unii(cur));  // whole node: 2x s_load_dwordx16 (4-wide)
-#endif
+            const NodeS nd = load_node_at(nbase, unii(cur));  // whole node: 2x s_load_dwordx16
             const float tc = fminf(fminf(thi, kt[KB - 1]), tcut);
-            float ent[BVH_W];
             uint64_t bal[BVH_W];
-#if GVRT_NODE64
-            // plane distance = (origin + offset - o) / d = offset * inv + (origin * inv - o * inv)
-            const float bxo = fmaf(h16lo((uint32_t)nd[12]), inv.x, -oinv.x);
-            const float byo = fmaf(h16hi((uint32_t)nd[12]), inv.y, -oinv.y);
-            const float bzo = fmaf(h16lo((uint32_t)nd[13]), inv.z, -oinv.z);
-#pragma unroll
-            for (int k = 0; k < BVH_W; ++k) {
-                const uint32_t wx = (uint32_t)nd[3 * k], wy = (uint32_t)nd[3 * k + 1], wz = (uint32_t)nd[3 * k + 2];
-                const bool hit = box_hit_t(fmaf(h16lo(wx), inv.x, bxo), fmaf(h16hi(wx), inv.x, bxo),
-                                           fmaf(h16lo(wy), inv.y, byo), fmaf(h16hi(wy), inv.y, byo),
-                                           fmaf(h16lo(wz), inv.z, bzo), fmaf(h16hi(wz), inv.z, bzo), tlo, tc, ent[k]);
-                bal[k] = __builtin_amdgcn_ballot_w64(hit);
-            }
-            const uint32_t meta = (uint32_t)nd[13] >> 16;
-            const uint32_t vmask = (meta >> 4) & 15u;
-            const uint32_t inner = meta & 15u;
-            const uint32_t lslots = vmask & ~inner;
-            const uint32_t ibase = (uint32_t)nd[14], lbase = (uint32_t)nd[15];
-            uint32_t hm = 0;
-#pragma unroll
-            for (int k = 0; k < BVH_W; ++k) hm |= bal[k] ? (1u << k) : 0u;
-            hm &= vmask;  // empty slots hold zero boxes: never descended into
-            if constexpr (STATS) w_dead += hm == 0 ? 1u : 0u;
-            uint32_t leafmask = hm & ~inner;
-            uint32_t im = hm & inner;
-            int32_t next = -1;
-            // internal children are contiguous node ids, leaf children contiguous leaf slots (slot order)
-            auto chsel = [&](int k) { return (int32_t)(ibase + __popc(inner & ((1u << k) - 1u))); };
-            auto leafsel = [&](int k) { return (int32_t)(lbase + __popc(lslots & ((1u << k) - 1u))); };
-            if (im) {
-                const bool rev = (rsign >> ((meta >> 8) & 3u)) & 1u;
-#else
-            // (a per-octant min/max-free box test as 8 template copies of the loop measured within noise: +0.7 %;
-            // the octant node copies below keep one code path for all octants)
             if (octw) {
-#if GVRT_PK_NF
-#pragma unroll
-                for (int k = 0; k < BVH_W; ++k)
-                    bal[k] = __builtin_amdgcn_ballot_w64(box_hit_pk_nf<SLACK>(
-                        pf2{NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 1)}, pf2{NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 3)},
-                        pf2{NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 5)}, ixy, oxy, izo, tlo, tc));
-#else
                 // (an opaque copy of 1/d: otherwise the first child's plane FMAs, common to both tests, are hoisted
                 // above the branch and every min / max input after it gets a canonicalising v_max)
                 f3 iv = inv;
@@ -917,86 +589,54 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                     bal[k] = __builtin_amdgcn_ballot_w64(
                         box_hit_nf<SLACK>(NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 1),
                                           NODE_BOX(nd, k, 3), NODE_BOX(nd, k, 5), oinv, iv, tlo, tc));
-#endif
             } else {
 #pragma unroll
-            for (int k = 0; k < BVH_W; ++k) {
-#if GVRT_PK_BOX && !GVRT_ASM_NODE
-                const bool hit = box_hit_pk(nd.box[k], oinv, inv, tlo, tc, ent[k]);
-#else
-                const bool hit = box_hit<SLACK>(NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 1),
-                                         NODE_BOX(nd, k, 3), NODE_BOX(nd, k, 5), o, oinv, inv, tlo, tc, ent[k]);
-#endif
-                bal[k] = __builtin_amdgcn_ballot_w64(hit);  // compare result straight to an SGPR mask
-                if constexpr (!GVRT_SOFF) bal[k] &= amask;
-            }
+                for (int k = 0; k < BVH_W; ++k)  // compare results straight to SGPR masks
+                    bal[k] = __builtin_amdgcn_ballot_w64(
+                        box_hit<SLACK>(NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 1),
+                                       NODE_BOX(nd, k, 3), NODE_BOX(nd, k, 5), oinv, inv, tlo, tc));
             }
             int32_t ch[BVH_W];
 #pragma unroll
             for (int k = 0; k < BVH_W; ++k) ch[k] = unii(NODE_CHILD(nd, k));
             // ---- children in the node's stored order (in-order of the binary split), forward when the
             // first lane's ray points along +axis, else backward: a handful of SALU ops per node
-            // (the entry-distance sort below costs ~100)
+            // (sorting the hit children by the first hitting lane's entry distance cost ~100 SALU per node and
+            // visited more nodes: 2.79 vs 2.18 ms)
             uint32_t hm = 0;
 #pragma unroll
-            for (int k = 0; k < BVH_W; ++k) hm |= GVRT_HM_ASM ? nz_bit(bal[k], 1u << k) : (bal[k] ? (1u << k) : 0u);
-            if constexpr (STATS && !GVRT_DIAG_PAIRS) w_dead += hm == 0 ? 1u : 0u;
+            for (int k = 0; k < BVH_W; ++k) hm |= nz_bit(bal[k], 1u << k);
+            if constexpr (STATS) w_dead += hm == 0 ? 1u : 0u;
             const uint32_t inner = uni(NODE_PAD(nd, 1));
             uint32_t leafmask = hm & ~inner;
-#if GVRT_DIAG_PAIRS
-            // diagnostic (STATS build): w_dead counts node visits whose hit leaf children's (leaf, lane) pairs fit
-            // fewer 64-lane passes than leaves; w_late sums the leaf passes such compaction would save
-            if constexpr (STATS) {
-                uint32_t nl = 0, np = 0;
-#pragma unroll
-                for (int k = 0; k < BVH_W; ++k)
-                    if ((leafmask >> k) & 1u) {
-                        ++nl;
-                        np += (uint32_t)__builtin_popcountll(bal[k]);
-                    }
-                const uint32_t passes = (np + 63) / 64;
-                w_dead += (nl >= 2 && passes < nl) ? 1u : 0u;
-                w_late += nl - passes;
-            }
-#endif
             uint32_t im = hm & inner;
             int32_t next = -1;
-            auto chsel = [&](int k) { return GVRT_PICK(ch, k); };
-            auto leafsel = [&](int k) { return ~GVRT_PICK(ch, k); };
             if (im) {
                 const bool rev = (rsign >> uni(NODE_PAD(nd, 0))) & 1u;
-#endif
                 const int first = rev ? 31 - __clz(im) : __ffs(im) - 1;
-                next = chsel(first);
+                next = GVRT_PICK(ch, first);
                 im &= ~(1u << first);
                 while (im) {  // the next child in visiting order ends on top
                     const int k = rev ? __ffs(im) - 1 : 31 - __clz(im);
-                    push(chsel(k));
+                    push(GVRT_PICK(ch, k));
                     im &= ~(1u << k);
                 }
             } else if (sp > 0) {
                 next = pop();
             }
-            // (sorting the hit children by the first hitting lane's entry distance instead cost ~100 SALU
-            // per node and visited more nodes: 2.79 vs 2.18 ms)
             [[maybe_unused]] uint64_t t_leaf0 = 0;
             if constexpr (STATS) {
                 t_leaf0 = __builtin_amdgcn_s_memtime();
                 cyc_node += t_leaf0 - t_node0;
             }
-            // ---- leaves of this node (the k-buffer orders them); one rolled loop = one insertion
-            // site; the next leaf's record load is issued before the current leaf's tests
+            // ---- leaves of this node (the k-buffer orders them); one rolled loop = one insertion site
 #pragma unroll 1
             while (leafmask) {
                 const int k = __builtin_ctz(leafmask);
                 leafmask &= leafmask - 1;
                 const uint64_t bk = GVRT_PICK(bal, k);
-                const int32_t li = leafsel(k);  // leaf slot
-#if GVRT_SOFF || GVRT_NODE64
+                const int32_t li = ~GVRT_PICK(ch, k);  // leaf slot
                 const RenderRec rec = load_rec_at(recs_, unii(li));
-#else
-                const RenderRec rec = recs_[li];
-#endif
                 // split (SplitBLAS analogue): the piece's proxy id and cell; cell == ~0u admits every crossing
                 uint4 pa = make_uint4((uint32_t)li, 0xFFFFFFFFu, 0u, 0u);
                 if (aux_) pa = aux_[li];
@@ -1022,7 +662,6 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                                 ADAPTIVE ? kernel_scale(rec.density, a.kmin, a.kopts, a.kdeg) * SQRT3 : a.kernel_h;
                             float tn, tf;
                             ico_clip(ok, dk, hk, tn, tf);
-                            GVRT_TRACE_REC(trace_on, 1, gi, tn, tf, acc ? 1.0f : 0.0f, galpha, rounds);
                             if (tn <= tf) {
                                 const float al = acc ? galpha : -1.0f;
                                 // (an inclusive tmin exists only in LITERAL mode: the API refuses it otherwise)
@@ -1043,35 +682,16 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                                     // whose running sum reaches qneed is the last one composited; no
                                     // slot can reach it while the inserted total is still below
                                     qtot += tb < INF_DIST ? 2 * q : q;
-#if GVRT_TCUT
                                     if (__builtin_amdgcn_ballot_w64(qtot >= qneed)) {
                                     uint32_t qs = 0;
                                     float tt = INF_DIST;
-#if GVRT_TCUT_GROUPS
-                                    // in 8-slot groups; slots are sorted, so once every walking lane has its cut
-                                    // the later groups cannot lower it
-                                    bool more = true;
-#pragma unroll
-                                    for (int g = 0; g < KB; g += 8) {
-                                        if (more) {
-#pragma unroll
-                                            for (int i = g; i < (g + 8 < KB ? g + 8 : KB); ++i) {
-                                                qs += kid[i] & 0xFFu;
-                                                tt = fminf(tt, qs >= qneed ? kt[i] : INF_DIST);
-                                            }
-                                            more = __builtin_amdgcn_ballot_w64(tt == INF_DIST && qtot >= qneed) != 0;
-                                        }
-                                    }
-#else
 #pragma unroll
                                     for (int i = 0; i < KB; ++i) {
                                         qs += kid[i] & 0xFFu;
                                         tt = fminf(tt, qs >= qneed ? kt[i] : INF_DIST);
                                     }
-#endif
                                     tcut = fminf(tcut, tt);
                                     }
-#endif
                                   } else {
                                     kb_insert2<KB>(ta, tb, gi, al, kt, kid, ka);
                                     // Termination-aware cull distance: walking the sorted slots with the
@@ -1079,7 +699,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                                     // is the last one that can ever be composited (the loop ends there), so
                                     // nothing farther is needed.  The 1e-4 margin keeps the bound
                                     // conservative against ulp differences from the composite's arithmetic.
-                                    float Tp = s_T[wid][LL], tt = INF_DIST;
+                                    float Tp = s_T[LL], tt = INF_DIST;
                                     const float term_cut = a.min_transmittance * 0.9999f;
                         #pragma unroll
                                     for (int i = 0; i < KB; ++i) {
@@ -1106,20 +726,20 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
             if (kid[0] == INVALID_ID) {
                 active = false;
             } else {
-                float T = s_T[wid][LL];
-                float4 acc = s_acc[wid][LL];
-                float last = s_last[wid][LL];
+                float T = s_T[LL];
+                float4 acc = s_acc[LL];
+                float last = s_last[LL];
                 // FAST: a buffer that did not fill holds every admitted crossing of (tlo, thi] (nothing was
                 // culled by kt[K-1]; what tcut culled lies past the slot where T drops below
                 // minTransmittance).  Once they are composited nothing is left, so the next round that
                 // the reference's loop would trace (and find empty) is skipped.
-                const bool full = LITERAL || !GVRT_SKIP_EMPTY_ROUND || kid[KB - 1] != INVALID_ID;
-                // Slots in groups of CU (static indices inside a group, so no per-hit register shift);
-                // the buffer shifts down by CU between groups.  Per lane: stop at the first empty slot
+                const bool full = LITERAL || kid[KB - 1] != INVALID_ID;
+                // Slots in groups of CUN (static indices inside a group, so no per-hit register shift);
+                // the buffer shifts down by CUN between groups.  Per lane: stop at the first empty slot
                 // or once T <= minTransmittance (slots are sorted with the empty ones last, T only falls).
                 bool go = true;
                 // groups of 6 for the default FAST depth (fewer shifts; spill-free there), else 4
-                constexpr int CUN = (PACK && KB == 24) ? GVRT_COMP_UNROLL : 4;
+                constexpr int CUN = (PACK && KB == 24) ? COMP_GROUP : 4;
 #pragma unroll 1
                 for (int base = 0; base < KB; base += CUN) {
 #pragma unroll
@@ -1131,18 +751,15 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                         float halpha;
                         bool hacc;
                         hid = PACK ? (kid[j] >> 8) : kid[j];
-#if GVRT_SH_PREFETCH
                         // the SH address needs only the id: issue all 12 loads with the record's, one
-                        // memory round trip per hit instead of one per dependent chunk (with GVRT_SH_UNCOND the
-                        // first GVRT_SH_EARLY of them are consumed unconditionally, so they are not sunk behind
-                        // the accept branch; all 12 early spilled VGPRs)
+                        // memory round trip per hit instead of one per dependent chunk (the first SH_EARLY of
+                        // them are consumed unconditionally, so they are not sunk behind the accept branch)
                         float4 shv[12];
                         {
                             const float4* s4 = reinterpret_cast<const float4*>(sh_ + 48ull * hid);
 #pragma unroll
                             for (int q = 0; q < 12; ++q) shv[q] = s4[q];
                         }
-#endif
                         if constexpr (PACK) {
                             // processHit re-evaluates the response of the hit particle (per-lane record load)
                             const RenderRec rec = crecs_[hid];
@@ -1154,36 +771,25 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
                             halpha = ka[j];
                             hacc = ka[j] > 0.0f;
                         }
-                        GVRT_TRACE_REC(trace_on, 2, hid, kt[j], halpha, T, hacc ? 1.0f : 0.0f, rounds);
-                        float er = 0.f, eg = 0.f, eb = 0.f;  // SH terms of the first GVRT_SH_EARLY / 3 chunks
-#if GVRT_SH_PREFETCH
-                        if constexpr (GVRT_SH_UNCOND && PACK) {
+                        float er = 0.f, eg = 0.f, eb = 0.f;  // SH terms of the first SH_EARLY / 3 chunks
+                        if constexpr (PACK) {
 #pragma unroll
-                            for (int q = 0; q < GVRT_SH_EARLY / 3; ++q) {
+                            for (int q = 0; q < SH_EARLY / 3; ++q) {
                                 const float4 v0 = shv[3 * q], v1 = shv[3 * q + 1], v2 = shv[3 * q + 2];
-                                const float4 bq = s_basis[wid][q][LL];
+                                const float4 bq = s_basis[q][LL];
                                 er += bq.x * v0.x; eg += bq.x * v0.y; eb += bq.x * v0.z;
                                 er += bq.y * v0.w; eg += bq.y * v1.x; eb += bq.y * v1.y;
                                 er += bq.z * v1.z; eg += bq.z * v1.w; eb += bq.z * v2.x;
                                 er += bq.w * v2.y; eg += bq.w * v2.z; eb += bq.w * v2.w;
                             }
                         }
-#endif
                         if (hacc) {
                             const float weight = halpha * T;
                             float rr = er, rg = eg, rb = eb;
-#if GVRT_SH_PREFETCH
 #pragma unroll
-                            for (int q = (GVRT_SH_UNCOND && PACK) ? GVRT_SH_EARLY / 3 : 0; q < 4; ++q) {
+                            for (int q = PACK ? SH_EARLY / 3 : 0; q < 4; ++q) {
                                 const float4 v0 = shv[3 * q], v1 = shv[3 * q + 1], v2 = shv[3 * q + 2];
-#else
-                            const float4* s4 = reinterpret_cast<const float4*>(sh_ + 48ull * hid);
-                            // 16 coefficients x rgb = 12 float4, in 4 rolled chunks of 3 (few live VGPRs)
-#pragma unroll 1
-                            for (int q = 0; q < 4; ++q) {
-                                const float4 v0 = s4[3 * q], v1 = s4[3 * q + 1], v2 = s4[3 * q + 2];
-#endif
-                                const float4 bq = s_basis[wid][q][LL];
+                                const float4 bq = s_basis[q][LL];
                                 const float b0 = bq.x, b1 = bq.y, b2 = bq.z, b3 = bq.w;
                                 // coefficients 4q..4q+3: (v0.xyz) (v0.w v1.xy) (v1.zw v2.x) (v2.yzw)
                                 rr += b0 * v0.x; rg += b0 * v0.y; rb += b0 * v0.z;
@@ -1212,24 +818,25 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
 #pragma unroll
                     for (int i = KB - CUN; i < KB; ++i) kid[i] = INVALID_ID;
                 }
-                active = full && (last <= s_tmax[wid][LL]) && (T > a.min_transmittance);
-                s_last[wid][LL] = last;
-                s_T[wid][LL] = T;
-                s_acc[wid][LL] = acc;
+                active = full && (last <= s_tmax[LL]) && (T > a.min_transmittance);
+                s_last[LL] = last;
+                s_T[LL] = T;
+                s_acc[LL] = acc;
             }
         }
         if constexpr (STATS) cyc_comp += __builtin_amdgcn_s_memtime() - t_comp0;
     }
+#undef LL
 
     // ---------------- outputs (pixel coordinates and lane recomputed: kept live through the traversal
     // they were spilled to scratch)
     const int olane = lane_now();
-    const float4 acc = s_acc[wid][olane];
+    const float4 acc = s_acc[olane];
     const float cr = acc.x, cg = acc.y, cb = acc.z, calpha = acc.w;
-    const uint32_t pxy = s_pxy[wid][olane];
+    const uint32_t pxy = s_pxy[olane];
     const uint32_t opx = pxy & 0xFFFFu, opy = pxy >> 16;
     const bool ovalid = opx < a.width && opy < a.height && cam < a.ncams;
-    const uint64_t otile = a.perm ? (uint64_t)a.perm[blockIdx.x] : (uint64_t)blockIdx.x * WGW + (uint32_t)wid;
+    const uint64_t otile = a.perm ? (uint64_t)a.perm[blockIdx.x] : (uint64_t)blockIdx.x;
     if (ovalid) {
         const uint64_t pix = ((uint64_t)cam * a.height + opy) * a.width + opx;
         const uint64_t oi = a.packed ? otile * 64 + olane : pix;
@@ -1238,11 +845,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
             auto q8 = [](float f) -> uint32_t { return (uint32_t)(fminf(fmaxf(f, 0.0f), 1.0f) * 255.0f + 0.5f); };
             reinterpret_cast<uint32_t*>(rgba8_)[oi] = q8(cr) | (q8(cg) << 8) | (q8(cb) << 16) | (q8(calpha) << 24);
         }
-#if GVRT_EXP_TILECOST
-        if (hit_counts_) hit_counts_[oi] = (uint32_t)(__builtin_amdgcn_s_memtime() - exp_t0);
-#else
         if (hit_counts_) hit_counts_[oi] = (uint32_t)(calpha - a.alpha_init);
-#endif
         if (ray_dirs_) {
             const uint64_t di = a.ray_dirs_layout == 1
                                     ? ((uint64_t)cam * a.width * a.height + (uint64_t)opx * a.height + opy)
@@ -1258,7 +861,7 @@ __global__ __launch_bounds__(64 * GVRT_WG_WAVES, GVRT_RENDER_MIN_WAVES) void k_r
     if (a.tile_bucket && olane == 0) {
         // this tile's cost class, 4 per octave of its cycles, at its tile-list position (vector store and
         // atomic from lane 0)
-        const uint64_t cyc = __builtin_amdgcn_s_memtime() - s_t0[wid];
+        const uint64_t cyc = __builtin_amdgcn_s_memtime() - s_t0;
         const float lc = (float)TILE_CPO * (__log2f((float)cyc + 1.0f) - 10.0f);  // 1 k cycles: class 0
         const uint32_t b = (uint32_t)fminf(fmaxf(lc, 0.0f), (float)(TILE_BUCKETS - 1));
         a.tile_bucket[otile] = (uint8_t)b;
@@ -1306,22 +909,16 @@ __global__ __launch_bounds__(256) void k_unpack(const uint32_t* __restrict__ pac
 }  // namespace
 
 gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64_t nwaves, bool literal) {
-    uint64_t blocks = (nwaves + WGW - 1) / WGW;
+    uint64_t blocks = nwaves;
     if (!a.tiles)
-        blocks = (uint64_t)((((a.tiles_x + WG_TW - 1) / WG_TW) + ST_W - 1) / ST_W) *
-                 ((((a.tiles_y + WG_TH - 1) / WG_TH) + ST_H - 1) / ST_H) * (ST_W * ST_H) * a.ncams;
+        blocks = (uint64_t)((a.tiles_x + ST_W - 1) / ST_W) * ((a.tiles_y + ST_H - 1) / ST_H) * (ST_W * ST_H) * a.ncams;
     if (nwaves == 0 || blocks == 0) return GVRT_OK;
     if (blocks > 0x7FFFFFFFull) return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "too many tiles");
     const bool adaptive = (a.kopts & 1u) != 0;
-    const dim3 g((unsigned)blocks), b(64 * WGW);
+    const dim3 g((unsigned)blocks), b(64);
     // every pointer is its own __restrict__ argument: the uniform node / record loads can then be
     // proven unclobbered by the output stores and are emitted as scalar (s_load) loads
-#if GVRT_NODE64
-#define KNODES a.nodes64
-#else
-#define KNODES a.nodes
-#endif
-#define KARGS KNODES, a.recs, a.crecs, a.aux, a.sh, a.view_inv, a.tiles, a.rgba8, a.rgba32f, a.ray_dirs, a.hit_counts, a.stats
+#define KARGS a.nodes, a.recs, a.crecs, a.aux, a.sh, a.view_inv, a.tiles, a.rgba8, a.rgba32f, a.ray_dirs, a.hit_counts, a.stats
 #define GVRT_LAUNCH_SO(L, A, K, P, S, O)                                                                  \
     do {                                                                                                  \
         if (a.stats) hipLaunchKernelGGL((k_render<L, A, K, true, P, S, O>), g, b, 0, c->stream, a, KARGS);   \
@@ -1335,10 +932,9 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
         if (a.box_exact) GVRT_LAUNCH_SO(false, false, K, true, false, false);                        \
         else GVRT_LAUNCH_SO(false, false, K, true, true, false);                                     \
     } while (0)
-    // packed payload needs record ids below 2^24 - 1 (id << 8 | q, all-ones = empty slot)
-    // (GVRT_NO_PACK forces the unpacked path, which scenes of >= 2^24 - 1 survivors take, for testing)
-    static const bool no_pack = getenv("GVRT_NO_PACK") != nullptr;
-    const bool pack = a.nrecs < 0xFFFFFFu && !no_pack;
+    // packed payload needs record ids below 2^24 - 1 (id << 8 | q, all-ones = empty slot); the handle
+    // option GVRT_OPT_PACKED_KBUFFER = 0 forces the unpacked path, which larger scenes take, for testing
+    const bool pack = a.nrecs < 0xFFFFFFu && c->opt[GVRT_OPT_PACKED_KBUFFER] != 0;
     if (literal) {  // the reference's 16-slot k-buffer (MAX_HIT_PER_TRACE)
         if (adaptive) GVRT_LAUNCH(true, true, K_HITS, false);
         else GVRT_LAUNCH(true, false, K_HITS, false);
@@ -1367,25 +963,10 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
 #undef GVRT_LAUNCH
 #undef GVRT_LAUNCH_F
 #undef GVRT_LAUNCH_SO
+#undef KARGS
     GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;
 }
-
-#if GVRT_TRACE
-extern "C" int gvrt_debug_trace_set(unsigned long long pix) {
-    const unsigned int z = 0;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_trace_pix), &pix, sizeof(pix)) != hipSuccess) return -1;
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_trace_n), &z, sizeof(z)) == hipSuccess ? 0 : -1;
-}
-extern "C" int gvrt_debug_trace_get(float* out, int maxn) {
-    unsigned int n = 0;
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_trace_n), sizeof(n)) != hipSuccess) return -1;
-    const int m = (int)(n < 8192u ? n : 8192u) < maxn ? (int)(n < 8192u ? n : 8192u) : maxn;
-    if (m > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace), sizeof(float) * 8 * m) != hipSuccess) return -1;
-    return (int)n;
-}
-#endif
 
 // The next launch's dispatch order (a permutation of tile-list positions) from this launch's cost classes,
 // costliest class first.  Class counts and
@@ -1455,11 +1036,8 @@ gvrt_status gvrt_launch_tile_order(gvrt_context* c) {
     const uint32_t p = c->ord_parity;
     uint32_t* h = c->d_thist;  // [hist 0, hist 1, fill 0, fill 1] x TILE_BUCKETS
     const uint32_t n = (uint32_t)c->ord_n;
-    // XCD-aware dealing of each cost class (GVRT_TILE_XCD=0: off): -2 to -4 % kernel time
-    static const uint32_t xcd = [] {
-        const char* e = getenv("GVRT_TILE_XCD");
-        return (uint32_t)!(e && e[0] == '0');
-    }();
+    // XCD-aware dealing of each cost class (GVRT_OPT_TILE_XCD = 0: off): -2 to -4 % kernel time
+    const uint32_t xcd = c->opt[GVRT_OPT_TILE_XCD] != 0;
     hipLaunchKernelGGL(k_tile_order, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, c->d_tbucket,
                        h + TILE_BUCKETS * p, h + TILE_BUCKETS * (2 + p), h + TILE_BUCKETS * (1 - p),
                        h + TILE_BUCKETS * (3 - p), c->d_order, xcd);
@@ -1532,10 +1110,6 @@ __global__ __launch_bounds__(256) void k_node_octants(uint64_t n, const Bvh4Node
 }
 
 gvrt_status gvrt_launch_node_octants(gvrt_context* c) {
-#if GVRT_NODE64 || GVRT_BVH_W != 4
-    (void)c;
-    return GVRT_OK;
-#else
     const uint64_t n = c->n_nodes4;
     if (!n || !c->d_nodes4) return GVRT_OK;
     // 8 x the node array (0.46 GB at 1 M Gaussians); when it does not fit, waves read the plain nodes
@@ -1548,7 +1122,6 @@ gvrt_status gvrt_launch_node_octants(gvrt_context* c) {
                        c->d_nodes4x8);
     GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;
-#endif
 }
 
 gvrt_status gvrt_launch_unpack(gvrt_context* c, const void* packed, const uint32_t* tiles, uint64_t ntiles,

@@ -402,6 +402,21 @@ void Camera::setLookAt(const gm::vec3& eye, const gm::vec3& target, const gm::ve
 }
 
 // ================================================================================== vks::Benchmark
+// Benchmark::run / saveResults follow base/benchmark.hpp:37-104 of the reference closely (the fps.txt and console
+// output are checked byte for byte against it, tests/test_host_cpp.py).  That file carries this notice:
+//   Benchmark class
+//   Copyright (C) 2016-2017 by Sascha Willems - www.saschawillems.de
+//   This code is licensed under the MIT license (MIT) (http://opensource.org/licenses/MIT)
+// MIT license text: Permission is hereby granted, free of charge, to any person obtaining a copy of this software
+// and associated documentation files (the "Software"), to deal in the Software without restriction, including
+// without limitation the rights to use, copy, modify, merge, publish, distribute, sublicense, and/or sell copies of
+// the Software, and to permit persons to whom the Software is furnished to do so, subject to the following
+// conditions: The above copyright notice and this permission notice shall be included in all copies or substantial
+// portions of the Software.  THE SOFTWARE IS PROVIDED "AS IS", WITHOUT WARRANTY OF ANY KIND, EXPRESS OR IMPLIED,
+// INCLUDING BUT NOT LIMITED TO THE WARRANTIES OF MERCHANTABILITY, FITNESS FOR A PARTICULAR PURPOSE AND
+// NONINFRINGEMENT. IN NO EVENT SHALL THE AUTHORS OR COPYRIGHT HOLDERS BE LIABLE FOR ANY CLAIM, DAMAGES OR OTHER
+// LIABILITY, WHETHER IN AN ACTION OF CONTRACT, TORT OR OTHERWISE, ARISING FROM, OUT OF OR IN CONNECTION WITH THE
+// SOFTWARE OR THE USE OR OTHER DEALINGS IN THE SOFTWARE.
 namespace vks {
 
 void Benchmark::run(std::function<void()> renderFunc, gvrt_device_properties props) {  // benchmark.hpp:37-75

@@ -136,6 +136,15 @@ class Renderer:
         self.build_accel(split_cells=split_cells, builder=builder, collapse=collapse)
         return m
 
+    def set_option(self, name, value):
+        """gvrt_set_option: a per-handle tuning switch by name (_lib.OPTIONS), 0 or 1."""
+        check(lib().gvrt_set_option(self.h, _lib.OPTIONS[name], int(value)), self.h)
+
+    def get_option(self, name):
+        v = C.c_int64(0)
+        check(lib().gvrt_get_option(self.h, _lib.OPTIONS[name], C.byref(v)), self.h)
+        return int(v.value)
+
     def set_stats(self, on=True):
         check(lib().gvrt_set_stats(self.h, 1 if on else 0), self.h)
 

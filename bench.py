@@ -412,8 +412,8 @@ def main():
                        "gaussians": n_input, "survivors": m, "width": W, "height": H,
                        "views": views, "split": args.split, "parallelism": f"{args.split}{world}",
                        "dispatch": "tiles costliest-first by the previous frame's per-tile cost, each cost class "
-                                   "dealt to the 8 XCDs in contiguous chunks (GVRT_TILE_ORDER=0: supertile order; "
-                                   "GVRT_TILE_XCD=0: no dealing)",
+                                   "dealt to the 8 XCDs in contiguous chunks (handle options tile_order=0: supertile order; "
+                                   "tile_xcd=0: no dealing)",
                        "build": ("quality: device binned-SAH tree + SAH-optimal 4-wide collapse" if args.build == "quality"
                                  else "fast: device LBVH + greedy 4-wide collapse")},
             "fps": round(1e3 / ms_per_step, 2),

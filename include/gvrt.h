@@ -31,6 +31,7 @@ typedef int32_t gvrt_status;
 #define GVRT_ERR_NO_DEVICE (-5)
 #define GVRT_ERR_IO (-6)
 #define GVRT_ERR_UNSUPPORTED (-7)
+#define GVRT_ERR_RCCL (-8) /* a collective of the multi-GPU frame exchange failed (host/gvrt_host.h GvrtApp) */
 
 typedef struct gvrt_context* gvrt_handle;
 
@@ -244,6 +245,22 @@ typedef struct {
     const float* particle_sph;        /* 48m SH records */
 } gvrt_device_buffers;
 gvrt_status gvrt_get_device_buffers(gvrt_handle h, gvrt_device_buffers* out);
+
+/* Per-handle tuning switches: the measured-best defaults; each exists so that a same-box
+ * A/B can turn one choice off.  None of them changes an image. */
+#define GVRT_OPT_TILE_ORDER 0u      /* 1 (default): tiles dispatched costliest first by the previous launch's
+                                       per-tile costs; 0: supertile order */
+#define GVRT_OPT_TILE_XCD 1u        /* 1 (default): each cost class dealt to the 8 XCDs in contiguous chunks */
+#define GVRT_OPT_OCTANT_NODES 2u    /* 1 (default): waves read the octant copy of the nodes (8x node memory) */
+#define GVRT_OPT_RECORD_ORIGINS 3u  /* 1 (default): single-origin FAST launches read kernel-frame origins
+                                       written into the leaf records by one pass per camera origin */
+#define GVRT_OPT_BOX_SLACK 4u       /* 0 (default): per-child exit slack only when the box padding does not
+                                       cover the plane rounding for the launch's cameras; 1: always */
+#define GVRT_OPT_PACKED_KBUFFER 5u  /* 1 (default): packed FAST k-buffer when record ids fit 24 bits; 0: the
+                                       unpacked FAST kernel that larger scenes take */
+#define GVRT_OPT_COUNT 6u
+gvrt_status gvrt_set_option(gvrt_handle h, uint32_t option, int64_t value);
+gvrt_status gvrt_get_option(gvrt_handle h, uint32_t option, int64_t* value);
 
 /* Enable per-render statistics (crossings/accepted/rounds; costs one atomic per wave). */
 gvrt_status gvrt_set_stats(gvrt_handle h, int enable);

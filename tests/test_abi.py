@@ -86,6 +86,28 @@ def test_no_device_is_a_status_not_an_abort(gv):
     props = L.DeviceProperties()
     assert gv.lib().gvrt_get_device_properties(0, C.byref(props)) == -5
     assert gv.lib().gvrt_get_device_buffers(None, C.byref(L.DeviceBuffers())) == -1
+    assert gv.lib().gvrt_set_option(None, 0, 1) == -1
+    v = C.c_int64(7)
+    assert gv.lib().gvrt_get_option(None, 0, C.byref(v)) == -1 and v.value == 7
+
+
+def test_option_names_match_header(gv):
+    """_lib.OPTIONS mirrors the GVRT_OPT_* values of include/gvrt.h."""
+    from importlib import import_module
+    L = import_module("3dgvrt_lightfield_amd._lib")
+    txt = open(HDR).read()
+    opts = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"#define GVRT_OPT_([A-Z_]+) (\d+)u", txt)}
+    count = opts.pop("count")
+    assert opts == L.OPTIONS and count == len(opts)
+
+
+def test_lib_path_override_is_confined_to_the_package(tmp_path):
+    """GVRT_LIB_PATH may only name a libgvrt.so built under the package (A/B variant builds)."""
+    code = "import importlib; importlib.import_module('3dgvrt_lightfield_amd._lib')"
+    for bad in (str(tmp_path / "libgvrt.so"), "/usr/lib/libm.so.6"):
+        r = subprocess.run(["python3", "-c", code], cwd=ROOT, capture_output=True, text=True,
+                           env=dict(os.environ, GVRT_LIB_PATH=bad))
+        assert r.returncode != 0 and "only a libgvrt.so built under" in r.stderr
 
 
 def test_ply_roundtrip_and_reorder(gv, tmp_path):

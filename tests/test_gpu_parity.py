@@ -481,24 +481,34 @@ def test_bicycle_subset_vs_oracle_and_fast_literal(gv, O, bicycle):
 
 def test_unpacked_fast_path_matches(gv, config1):
     """Scenes with >= 2^24 - 1 survivors cannot use the packed (id << 8 | q) k-buffer payload and run
-    the unpacked FAST kernel; GVRT_NO_PACK forces that path on a small scene (read per process)."""
-    import os
-    import subprocess
-    import sys
-    code = (
-        "import importlib, numpy as np, sys; gv = importlib.import_module('3dgvrt_lightfield_amd');"
-        "s = gv.scene.config1(); vi, pi = gv.scene.config1_camera(96, 96);"
-        "r = gv.Renderer(0); r.prepare(s); o = r.render(vi, pi, 96, 96)['rgba32f'];"
-        "np.save(sys.argv[1], o)")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    the unpacked FAST kernel; the handle option packed_kbuffer = 0 forces that path on a small scene."""
+    vi, pi = gv.scene.config1_camera(96, 96)
     outs = []
-    for env_extra, name in (({}, "packed"), ({"GVRT_NO_PACK": "1"}, "unpacked")):
-        path = os.path.join(root, "gpurun_out", f"pack_{name}.npy")
-        os.makedirs(os.path.dirname(path), exist_ok=True)
-        env = dict(os.environ, **env_extra)
-        subprocess.run([sys.executable, "-c", code, path], check=True, cwd=root, env=env, timeout=300)
-        outs.append(np.load(path))
-        os.remove(path)
+    for packed in (1, 0):
+        with gv.Renderer(0) as r:
+            r.set_option("packed_kbuffer", packed)
+            r.prepare(config1)
+            outs.append(r.render(vi, pi, 96, 96)["rgba32f"])
     # same crossings, same order; alpha is computed at insert time (unpacked) or re-evaluated at
     # composite time (packed) by the same function: the images agree to float rounding
     np.testing.assert_allclose(outs[0], outs[1], rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("option", ["tile_order", "tile_xcd", "octant_nodes", "record_origins", "box_slack"])
+def test_tuning_options_change_no_pixel(gv, config1, option):
+    """Each per-handle tuning switch (gvrt_set_option) changes how the frame is computed, never a pixel:
+    the frame with the switch flipped equals the default frame bit for bit (two launches each, so the
+    cost-ordered dispatch of the second launch is covered too)."""
+    W, H = 200, 136
+    vi, pi = gv.scene.config1_camera(W, H)
+    with gv.Renderer(0) as r:
+        r.prepare(config1)
+        ref = [r.render(vi, pi, W, H)["rgba32f"] for _ in range(2)]
+        default = r.get_option(option)
+        r.set_option(option, 1 - default)
+        assert r.get_option(option) == 1 - default
+        got = [r.render(vi, pi, W, H)["rgba32f"] for _ in range(2)]
+        with pytest.raises(gv.GvrtError):
+            r.set_option(option, 2)
+    for a, b in zip(ref, got):
+        np.testing.assert_array_equal(a, b)
