@@ -140,6 +140,9 @@ gvrt_status gvrt_destroy(gvrt_handle c) {
     for (void* p : ptrs) (void)hipFree(p);
     c->allocs.clear();
     for (hipEvent_t e : c->async_ev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->cam_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->h_viewinv_pin) (void)hipHostFree(c->h_viewinv_pin);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -470,6 +473,29 @@ static gvrt_status ensure_tile_order(gvrt_context* c, uint32_t tiles_x, uint32_t
     return GVRT_OK;
 }
 
+// The camera ring sized for ncams cameras per slot (regrown, after the queued frames, when a launch has more).
+static gvrt_status ensure_cameras(gvrt_context* c, uint32_t ncams) {
+    if (c->cam_stride >= 16ull * ncams && c->d_viewinv) return GVRT_OK;
+    GVRT_HIP(c, hipStreamSynchronize(c->stream));  // queued frames read the old ring
+    gvrt_dfree(c, (void**)&c->d_viewinv);
+    if (c->h_viewinv_pin) {
+        (void)hipHostFree(c->h_viewinv_pin);
+        c->h_viewinv_pin = nullptr;
+    }
+    c->cam_stride = 0;
+    c->cam_valid = false;
+    for (uint32_t i = 0; i < gvrt_context::CAM_RING; ++i) {
+        if (!c->cam_ev[i]) GVRT_HIP(c, hipEventCreateWithFlags(&c->cam_ev[i], hipEventDisableTiming));
+        c->cam_ev_live[i] = false;
+    }
+    const uint64_t stride = 16ull * std::max<uint32_t>(ncams, 4);
+    gvrt_status s;
+    if ((s = gvrt_dalloc(c, (void**)&c->d_viewinv, 4 * stride * gvrt_context::CAM_RING))) return s;
+    GVRT_HIP(c, hipHostMalloc((void**)&c->h_viewinv_pin, 4 * stride * gvrt_context::CAM_RING, hipHostMallocDefault));
+    c->cam_stride = stride;
+    return GVRT_OK;
+}
+
 static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const float* view_inverse,
                                const float* proj_inverse, uint32_t width, uint32_t height, uint32_t ncams,
                                const gvrt_tile* tiles, uint64_t ntiles, const gvrt_image* out, bool async) {
@@ -513,17 +539,23 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
     // the render kernel addresses leaf records (64 B) and 4-wide nodes (128 B) by 32-bit byte offsets
     if (c->n_leaves >= (1ull << 26) || c->n_nodes4 >= (1ull << 25))
         return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "more than 2^26 BVH leaves or 2^25 nodes (32-bit record offsets)");
-    // cameras
-    if ((s = ensure(c, (void**)&c->d_viewinv, &c->viewinv_cap, 64ull * ncams))) return s;
-    // the camera matrices go up only when they changed (a pageable 64-B upload costs a host round trip
-    // per frame for a static camera)
-    if (c->h_viewinv.size() != 16ull * ncams ||
+    // cameras: uploaded only when they changed, into the next slot of the device ring, so that a moving camera
+    // costs no host round trip per frame (the slot's previous reader has long finished: its event is waited for
+    // only if the queue is CAM_RING frames deep)
+    if ((s = ensure_cameras(c, ncams))) return s;
+    if (!c->cam_valid || c->h_viewinv.size() != 16ull * ncams ||
         std::memcmp(c->h_viewinv.data(), view_inverse, 64ull * ncams) != 0) {
-        if (c->async_pending) GVRT_HIP(c, hipStreamSynchronize(c->stream));  // an async upload may still read it
+        const uint32_t slot = (c->cam_slot + 1) % gvrt_context::CAM_RING;
+        if (c->cam_ev_live[slot]) GVRT_HIP(c, hipEventSynchronize(c->cam_ev[slot]));
+        float* src = c->h_viewinv_pin + slot * c->cam_stride;
+        std::memcpy(src, view_inverse, 64ull * ncams);
+        GVRT_HIP(c, hipMemcpyAsync(c->d_viewinv + slot * c->cam_stride, src, 64ull * ncams, hipMemcpyHostToDevice,
+                                   c->stream));
         c->h_viewinv.assign(view_inverse, view_inverse + 16ull * ncams);
-        GVRT_HIP(c, hipMemcpyAsync(c->d_viewinv, c->h_viewinv.data(), 64ull * ncams, hipMemcpyHostToDevice, c->stream));
+        c->cam_slot = slot;
+        c->cam_valid = true;
     }
-    a.view_inv = c->d_viewinv;
+    a.view_inv = c->d_viewinv + c->cam_slot * c->cam_stride;
     std::memcpy(a.proj_inv, proj_inverse, 64);
     std::memcpy(a.aabb, p->aabb, 24);
     a.min_transmittance = p->min_transmittance;
@@ -649,6 +681,8 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         GVRT_HIP(c, hipEventRecord(e0, c->stream));
         if ((s = gvrt_launch_render_mode(c, a, nwork, p->mode == GVRT_MODE_LITERAL))) return s;
         GVRT_HIP(c, hipEventRecord(e1, c->stream));
+        GVRT_HIP(c, hipEventRecord(c->cam_ev[c->cam_slot], c->stream));
+        c->cam_ev_live[c->cam_slot] = true;
         if (ordered && (s = gvrt_launch_tile_order(c))) return s;
         ++c->async_pending;
         c->stats.rays = (tiles || out->packed) ? nwork * 64 : total_tiles * 64;
@@ -658,6 +692,8 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
     GVRT_HIP(c, hipEventRecord(c->ev0, c->stream));
     if ((s = gvrt_launch_render_mode(c, a, nwork, p->mode == GVRT_MODE_LITERAL))) return s;
     GVRT_HIP(c, hipEventRecord(c->ev1, c->stream));
+    GVRT_HIP(c, hipEventRecord(c->cam_ev[c->cam_slot], c->stream));
+    c->cam_ev_live[c->cam_slot] = true;
     if (ordered && (s = gvrt_launch_tile_order(c))) return s;
     if (!out->device_ptrs) {
         if (b32) GVRT_HIP(c, hipMemcpyAsync(out->rgba32f, a.rgba32f, b32, hipMemcpyDeviceToHost, c->stream));

@@ -72,9 +72,17 @@ struct gvrt_context {
     unsigned long long* d_stats = nullptr;
     uint32_t* d_tiles = nullptr;
     uint64_t tiles_cap = 0;
-    float* d_viewinv = nullptr;
-    uint64_t viewinv_cap = 0;
-    std::vector<float> h_viewinv;  // host copy of what d_viewinv holds
+    // camera matrices: a ring of CAM_RING slots in device memory, filled from a pinned host mirror, so that a
+    // camera that changes every frame (a moving camera) is uploaded without waiting for the queued frames
+    static constexpr uint32_t CAM_RING = 16;
+    float* d_viewinv = nullptr;      // CAM_RING slots of cam_stride floats
+    float* h_viewinv_pin = nullptr;  // pinned host mirror of the ring (the source of the stream-ordered uploads)
+    uint64_t cam_stride = 0;         // floats per slot (16 x the largest camera count so far)
+    uint32_t cam_slot = 0;           // the slot holding the current cameras
+    bool cam_valid = false;          // cam_slot holds h_viewinv
+    hipEvent_t cam_ev[CAM_RING] = {};  // recorded after the last launch that read each slot
+    bool cam_ev_live[CAM_RING] = {};
+    std::vector<float> h_viewinv;    // the cameras in cam_slot
     std::vector<uint32_t> h_tiles; // host copy of what d_tiles holds (uploaded only when the list changes)
     bool tiles_valid = false;      // d_tiles holds h_tiles
     // gvrt_unpack_tiles_rgba8's lists (own buffers: queued renders may read d_tiles): one per rank part of a

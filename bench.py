@@ -65,6 +65,14 @@ def parse():
     ap.add_argument("--exchange", action="store_true",
                     help="run the multi-GPU frame-exchange path even with one rank (torch.distributed.run "
                          "--nproc-per-node 1: rehearses the N-rank step on one GPU)")
+    ap.add_argument("--camera-path", default="static", choices=["static", "orbit"],
+                    help="static: every frame renders the config camera (the headline); orbit: the camera's azimuth "
+                         "advances by --orbit-step degrees per frame (a moving camera: the reference's frame loop "
+                         "updates the camera every frame, base/VulkanRTBase.cpp:395-440, base/camera.hpp:229-281)")
+    ap.add_argument("--orbit-step", type=float, default=0.5, help="degrees of azimuth per frame (--camera-path orbit)")
+    ap.add_argument("--rank-balance", type=int, default=0,
+                    help="one GPU only: also time each of N ranks' parts of the split (tile lists of --split tiles, "
+                         "view groups of --split views) as that rank would render it, and report the imbalance")
     ap.add_argument("--build", default="quality", choices=["quality", "fast"],
                     help="quality: device binned-SAH tree + SAH-optimal 4-wide collapse (the static-scene build, "
                          "as the reference's PREFER_FAST_TRACE BLAS); fast: device LBVH + greedy collapse")
@@ -148,6 +156,46 @@ def pmc_passes(args):
     return out
 
 
+def rank_balance(args, r, gv, dist_mod, vi_all, pi, W, H, views, params, full_ms, reps=4):
+    """Strong-scaling imbalance measured on one GPU: each of N ranks' parts of the split rendered alone, as that
+    rank renders it (its own cost-ordered dispatch: the part is rendered `reps` times, the first launch of a
+    list being unordered, and the later ones' median kept).  Tile split: the 64x64-block round-robin tile
+    lists of dist.rank_tiles; view split: dist.rank_views of the rig.  implied_efficiency = full-workload
+    kernel time / (N x slowest part): the N-GPU efficiency this imbalance allows (gather not included)."""
+    import torch
+    n = args.rank_balance
+    dev = torch.device("cuda", 0)
+    ms = []
+    if args.split == "tiles":
+        parts = dist_mod.rank_tiles(W, H, 1, n, block=8)
+        buf = torch.zeros((max(t.shape[0] for t in parts) * 64, 4), dtype=torch.uint8, device=dev)
+        for t in parts:
+            got = []
+            for _ in range(reps):
+                r.render_device(vi_all[:16], pi, W, H, 1, params=params, tiles=t, rgba8_ptr=buf.data_ptr(), packed=True)
+                got.append(r.render_ms())
+            ms.append(float(np.median(got[1:])))
+        what = f"{n} tile lists (64x64-pixel blocks round-robin), {parts[0].shape[0]}..{parts[-1].shape[0]} tiles each"
+    else:
+        groups = dist_mod.rank_views(views, n)
+        vis = np.asarray(vi_all, np.float32).reshape(-1, 16)
+        buf = torch.zeros((max(len(g) for g in groups), H, W, 4), dtype=torch.uint8, device=dev)
+        for g in groups:
+            if not g:
+                continue
+            got = []
+            for _ in range(reps):
+                r.render_device(np.ascontiguousarray(vis[g].reshape(-1)), pi, W, H, len(g), params=params,
+                                rgba8_ptr=buf.data_ptr())
+                got.append(r.render_ms())
+            ms.append(float(np.median(got[1:])))
+        what = f"{n} view groups of the {views}-view rig ({len(groups[0])} views each)"
+    mean, mx = float(np.mean(ms)), float(np.max(ms))
+    return {"ranks": n, "parts": what, "kernel_ms": [round(x, 4) for x in ms], "max_over_mean": round(mx / mean, 4),
+            "full_kernel_ms": round(full_ms, 4), "implied_efficiency": round(full_ms / (n * mx), 4),
+            "note": "each part alone on one GPU with its own cost-ordered dispatch; median of the ordered launches"}
+
+
 def main():
     args = parse()
     dist_mod = importlib.import_module("3dgvrt_lightfield_amd.dist")  # no GPU work at import
@@ -194,28 +242,36 @@ def main():
 
     # cameras: an N-view planar rig starting at the config camera (view 0 = the config camera for any N);
     # config 5 (lightfield) is its centred 16-view array
-    if args.config == "config1":
-        eye, fovy = (0.0, 0.0, 3.0), gv.camera.FOV_Y
-    else:
-        eye, fovy = gv.camera.orbit_eye(4.0, 20.0, 30.0), 50.0  # = scene.mipnerf_camera (view 0)
+    # --camera-path orbit: frame k's rig sits at azimuth 30 + k * orbit_step (the static headline: k = 0 always)
     views = world if args.split == "views" else 1
     views = max(views, ncams_cfg if args.config == "lightfield" else 1)
-    vis, pi = gv.camera.lightfield_grid_rig(eye, (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), nx=views, ny=1, spacing=0.1,
-                                            fovy_deg=fovy, aspect=gv.camera.aspect_ratio(W, H),
-                                            centred=args.config == "lightfield")
-    vis = vis.reshape(views, 16)
+
+    def rig(k):
+        if args.config == "config1":
+            eye, fovy = (0.0, 0.0, 3.0), gv.camera.FOV_Y
+        else:
+            az = 30.0 + (k * args.orbit_step if args.camera_path == "orbit" else 0.0)
+            eye, fovy = gv.camera.orbit_eye(4.0, 20.0, az), 50.0  # k = 0: scene.mipnerf_camera (view 0)
+        v, p = gv.camera.lightfield_grid_rig(eye, (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), nx=views, ny=1, spacing=0.1,
+                                             fovy_deg=fovy, aspect=gv.camera.aspect_ratio(W, H),
+                                             centred=args.config == "lightfield")
+        return v.reshape(views, 16), p
+
+    nframes = 1 + args.warmup + args.steps
+    rigs = [rig(k) for k in range(nframes)] if args.camera_path == "orbit" else [rig(0)] * nframes
+    vis, pi = rigs[0]
     mode = gv.MODE_FAST if args.mode == "fast" else gv.MODE_LITERAL
     params = r.render_params(mode=mode)
     if args.split == "views":
         all_views = dist_mod.rank_views(views, world)
         my_views = all_views[rank]
-        vi = np.ascontiguousarray(vis[my_views].reshape(-1))
+        frame_vi = [np.ascontiguousarray(v[my_views].reshape(-1)) for v, _ in rigs]
         ncams = len(my_views)
         tiles = None
         rays_per_rank = W * H * ncams
         part_sizes, item_shape = [len(v) for v in all_views], (H, W, 4)
     else:
-        vi = np.ascontiguousarray(vis[0])
+        frame_vi = [np.ascontiguousarray(v[0]) for v, _ in rigs]
         ncams = 1
         all_tiles = dist_mod.rank_tiles(W, H, 1, world, block=8)
         tiles = all_tiles[rank]
@@ -224,6 +280,12 @@ def main():
     packed = args.split == "tiles"
     kernel_ms = []
     full = None
+    frame_k = [0]  # frames rendered so far (frame_vi index)
+
+    def next_vi():
+        v = frame_vi[min(frame_k[0], nframes - 1)]
+        frame_k[0] += 1
+        return v
 
     if distributed:
         # one exchange step per frame: dist.FrameExchange, double-buffered RCCL gather to rank 0
@@ -246,8 +308,8 @@ def main():
                                     assemble=assemble, sync=None)
 
         def render_into(buf):
-            r.render_device(vi, pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=buf.data_ptr(), packed=packed,
-                            async_=True)
+            r.render_device(next_vi(), pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=buf.data_ptr(),
+                            packed=packed, async_=True)
 
         def step():
             ex.step(render_into)
@@ -262,13 +324,20 @@ def main():
         frame = torch.zeros((part_sizes[0],) + item_shape, dtype=torch.uint8, device=dev)
 
         def step():
-            r.render_device(vi, pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=frame.data_ptr(),
+            r.render_device(next_vi(), pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=frame.data_ptr(),
                             packed=packed, async_=True)
 
         def drain():
             r.sync()
             kernel_ms.append(r.render_ms())  # mean over the queued launches
 
+    # the first frame of a frame size has no previous per-tile costs: it is dispatched in supertile order
+    # (frame 0, rendered synchronously and timed on its own; the handle orders every later frame)
+    first_buf = torch.zeros((part_sizes[0],) + item_shape, dtype=torch.uint8, device=dev)
+    r.render_device(next_vi(), pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=first_buf.data_ptr(),
+                    packed=packed)
+    first_frame_ms = r.render_ms()
+    del first_buf
     for _ in range(args.warmup):
         step()
     drain()
@@ -317,6 +386,7 @@ def main():
         # ---- roofline: algorithmic bytes of the reference algorithm on this input (LITERAL counters)
         roof = None
         lit_stats = None
+        vi = frame_vi[0]  # the frame-0 camera (the static headline's) for the counters and the CPU baseline
         if not args.no_stats:
             r.set_stats(True)
             r.render(vi[:16], pi, W, H, 1, params=r.render_params(mode=gv.MODE_LITERAL), rgba8=False, rgba32f=False)
@@ -392,6 +462,9 @@ def main():
                              "frac_beyond_1e-4_off_threshold": float((d[~amb] > 1e-4).mean()) if (~amb).any() else 0.0,
                              "frac_beyond_1e-4_all": float((d > 1e-4).mean())}
 
+        balance = rank_balance(args, r, gv, dist_mod, frame_vi[0], pi, W, H, views, params, kern_avg) \
+            if args.rank_balance > 1 and world == 1 else None
+
         result = {
             "metric": "Mrays/s + fps @1920x1080, 1M Gaussians; PSNR vs Vulkan reference",
             "value": round(mrays, 3),
@@ -421,6 +494,10 @@ def main():
             "kernel_mrays": round(rays_per_rank / (kern_avg * 1e-3) / 1e6, 3) if kern_avg == kern_avg else None,
             "psnr_vs_oracle_db": None if psnr is None else (round(psnr, 2) if math.isfinite(psnr) else "inf"),
             "frame_sha1": digest,
+            "camera_path": (f"orbit: azimuth 30 + {args.orbit_step} deg per frame (every frame a new camera; the "
+                            f"cost order of each frame from its predecessor)" if args.camera_path == "orbit"
+                            else "static: every frame the config camera"),
+            "first_frame_kernel_ms": round(first_frame_ms, 4),
             "enclose_ms": round(st0["enclose_ms"], 3),
             "accel_ms": round(st0["accel_ms"], 3),
             "first_build_ms": round(first_build["enclose_ms"] + first_build["accel_ms"], 3),
@@ -428,6 +505,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if balance:
+            result["rank_balance"] = balance
         if lit_stats:
             result["reference_counters"] = {"crossings_per_ray": lit_stats["crossings"] / (W * H),
                                             "accepted_per_ray": lit_stats["accepted"] / (W * H),

@@ -237,7 +237,7 @@ struct RayState {
 };
 
 bool processHit(const Scene& s, V3 o, V3 d, uint32_t idx, float minKernelDensity, float minAlpha,
-                uint32_t sphEvalDegree, RayState& st, HitEval* eval = nullptr) {
+                uint32_t sphEvalDegree, RayState& st, HitEval* eval = nullptr, float* radmax = nullptr) {
     const float* rec = s.density + 12ull * idx;
     const V3 pos = v3(rec[0], rec[1], rec[2]);
     const float dens = rec[3];
@@ -264,6 +264,7 @@ bool processHit(const Scene& s, V3 o, V3 d, uint32_t idx, float minKernelDensity
         const float* shp = s.sh + 48ull * idx;  // fetchParticleSphCoefficients :104-115
         for (int i = 0; i < 16; ++i) c[i] = v3(shp[3 * i], shp[3 * i + 1], shp[3 * i + 2]);
         const V3 grad = radianceFromSpH(sphEvalDegree, c, d, true);
+        if (radmax) *radmax = std::max(*radmax, std::max(grad.x, std::max(grad.y, grad.z)));
         st.rad[0] += grad.x * weight;
         st.rad[1] += grad.y * weight;
         st.rad[2] += grad.z * weight;
@@ -273,6 +274,19 @@ bool processHit(const Scene& s, V3 o, V3 d, uint32_t idx, float minKernelDensity
     }
     return acceptHit;
 }
+
+// largest colour channel of particle idx's radiance along d (parity accounting: the colour a flipped decision moves)
+float radianceMax(const Scene& s, uint32_t idx, V3 d, uint32_t sphEvalDegree) {
+    V3 c[16];
+    const float* shp = s.sh + 48ull * idx;
+    for (int i = 0; i < 16; ++i) c[i] = v3(shp[3 * i], shp[3 * i + 1], shp[3 * i + 2]);
+    const V3 r = radianceFromSpH(sphEvalDegree, c, d, true);
+    return std::max(r.x, std::max(r.y, r.z));
+}
+
+// Thresholds of the parity accounting (oracle/oracle.py THR_EPS, PAIR_EPS, BOUND_EPS must equal these:
+// oracle_flag_eps, tests/test_oracle_kat.py)
+constexpr float FLAG_THR_EPS = 1e-4f, FLAG_PAIR_EPS = 2e-6f, FLAG_BOUND_EPS = 1e-5f;
 
 // ---------------------------------------------------------------- CPU BVH over proxies
 struct BNode {
@@ -453,7 +467,14 @@ typedef struct {
     float kernel_degree;
 } oracle_params;
 
-int oracle_version(void) { return 3; }
+int oracle_version(void) { return 4; }
+
+// the parity accounting's flag thresholds (oracle.py THR_EPS, PAIR_EPS, BOUND_EPS)
+void oracle_flag_eps(float* out3) {
+    out3[0] = FLAG_THR_EPS;
+    out3[1] = FLAG_PAIR_EPS;
+    out3[2] = FLAG_BOUND_EPS;
+}
 
 // particlePrimitives.comp:112-215, with deterministic compaction (saveIdx = rank among
 // survivors in input order; the reference's atomicAdd order is nondeterministic, Q3) and
@@ -560,7 +581,7 @@ static thread_local std::vector<float>* g_trace = nullptr;
 
 // The per-ray ray-march: particleRendering.comp:117-191 (RQ) / raygen.rgen:303-383 (RT).
 // out_stats[3*r] = processed crossings (X_r), [3r+1] = accepted (A_r), [3r+2] = rounds.
-// out_margin[3*r .. 3*r+2] (optional; parity accounting, not part of the reference algorithm): how
+// out_margin[4*r .. 4*r+3] (optional; parity accounting, not part of the reference algorithm): how
 // close the ray came to a decision that a few-ulp different float evaluation (GPU exp / rsqrt / rcp,
 // FMA contraction) could take the other way.
 //   [0] relative distance to a threshold: |gres/hitMin - 1| and |galpha/alphaMin - 1| of every processed
@@ -572,7 +593,14 @@ static thread_local std::vector<float>* g_trace = nullptr;
 //       two accepted), the crossing that ends the ray (T <= minTransmittance) against its successor (if that
 //       one would be accepted), a ray grazing a proxy
 //       whose crossings would be accepted (relative chord |tout - tin| / |t|), and 0 for a crossing
-//       dropped because its t tied bitwise with `last` (the exclusive-tmin round boundary, Q13).
+//       dropped because its t tied bitwise with `last` (the exclusive-tmin round boundary, Q13);
+//   [3] flip bound: an upper bound on |d rgb| that the decisions flagged by [0..2] (below FLAG_*_EPS) can cause
+//       if a different float evaluation takes them the other way.  Each flagged decision moves the colour by at
+//       most (transmittance before it) x (opacity it moves) x (largest radiance channel involved): a threshold
+//       flip T_i a_i c, a swapped pair T_i a_i a_j |c_i - c_j|, a tie at a round / buffer / termination boundary
+//       T a c; the sum over the ray's flagged decisions, plus minTransmittance x c for the termination point the
+//       flip may move, with c the largest radiance channel of every crossing composited or flagged on the ray.
+//       0 for a ray with no flagged decision.
 struct OracleScene {
     Scene s;
     Bvh bvh;
@@ -681,6 +709,15 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
         float last = std::max(0.0f, tminb - EPS_T);
         Hit kb[MAX_HIT_PER_TRACE];
         float m_thr = INFINITY, m_t = INFINITY, m_b = INFINITY, prev_t = NAN, prev_acc_t = NAN;
+        // flip bound (out_margin[3]): summed T x alpha of the flagged decisions, the largest radiance channel
+        // involved, and the previous accepted crossing's T before it and alpha (pair swaps)
+        float fw = 0.0f, fc = 0.0f, prev_acc_T = 0.0f, prev_acc_a = 0.0f;
+        bool flagged = false;
+        auto flag = [&](float w, uint32_t id) {
+            flagged = true;
+            fw += w;
+            if (id != INVALID_PARTICLE_ID) fc = std::max(fc, radianceMax(s, id, d, P->sph_eval_degree));
+        };
         bool round_start = false;
         uint32_t prev_id = INVALID_PARTICLE_ID;
         std::vector<uint32_t> last_ids;  // ids processed with t == last (tie detection, out_margin)
@@ -690,6 +727,7 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
             if (P->max_rounds && rounds >= P->max_rounds) break;
             ++rounds;
             const float tmin = last + EPS_T, tmax = tmaxb + EPS_T;
+            const float T_round = st.T;
             for (uint32_t i = 0; i < MAX_HIT_PER_TRACE; ++i) kb[i] = Hit{INVALID_PARTICLE_ID, INFINITE_DISTANCE};
             Hit h_out{INVALID_PARTICLE_ID, INFINITE_DISTANCE};  // nearest crossing left out of a full buffer
             // ---- trace(): driver traversal + any-hit (anyhit.rahit:40-71)
@@ -697,8 +735,12 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                 const bool inRange = (P->tmin_inclusive ? t >= tmin : t > tmin) && t <= tmax;
                 if (!inRange) {
                     if (out_margin && t == last && t <= tmax &&
-                        std::find(last_ids.begin(), last_ids.end(), pid) == last_ids.end())
+                        std::find(last_ids.begin(), last_ids.end(), pid) == last_ids.end()) {
                         m_b = 0.0f;  // dropped only because its t ties with the last processed crossing
+                        const HitEval he = evalResponse(s, pid, o, d);
+                        if (he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min)
+                            flag(T_round * he.galpha, pid);
+                    }
                     return;
                 }
                 if (P->drop_rejected) {
@@ -748,8 +790,11 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                             // grazing the proxy: whether it is crossed at all is a few-ulp decision; it
                             // matters when its crossings would be composited
                             const HitEval he = evalResponse(s, g, o, d);
-                            if (he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min)
-                                m_b = std::min(m_b, std::fabs(tout - tin) / std::max(std::fabs(tin), 1e-30f));
+                            if (he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min) {
+                                const float gg = std::fabs(tout - tin) / std::max(std::fabs(tin), 1e-30f);
+                                m_b = std::min(m_b, gg);
+                                if (gg < FLAG_BOUND_EPS) flag(2.0f * T_round * he.galpha, g);
+                            }
                         }
                         if (crossed) {
                             anyhit(g, tin);
@@ -788,31 +833,60 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
             // (which of two tied crossings makes the round changes the image only if one of them is accepted)
             if (out_margin && kb[MAX_HIT_PER_TRACE - 1].id != INVALID_PARTICLE_ID && h_out.id != INVALID_PARTICLE_ID &&
                 gap(kb[MAX_HIT_PER_TRACE - 1].t, h_out.t) < 1e-4f &&
-                (accepted(kb[MAX_HIT_PER_TRACE - 1].id) || accepted(h_out.id)))
-                m_b = std::min(m_b, gap(kb[MAX_HIT_PER_TRACE - 1].t, h_out.t));
+                (accepted(kb[MAX_HIT_PER_TRACE - 1].id) || accepted(h_out.id))) {
+                const float gg = gap(kb[MAX_HIT_PER_TRACE - 1].t, h_out.t);
+                m_b = std::min(m_b, gg);
+                if (gg < FLAG_BOUND_EPS) {
+                    flag(T_round * evalResponse(s, kb[MAX_HIT_PER_TRACE - 1].id, o, d).galpha,
+                         kb[MAX_HIT_PER_TRACE - 1].id);
+                    flag(T_round * evalResponse(s, h_out.id, o, d).galpha, h_out.id);
+                }
+            }
             round_start = true;
             // ---- process k hits
             for (uint32_t i = 0; i < MAX_HIT_PER_TRACE; ++i) {
                 const Hit h = kb[i];
                 if (h.id != INVALID_PARTICLE_ID && st.T > P->min_transmittance) {
                     HitEval ev{0.0f, 0.0f};
+                    const float T_before = st.T;
                     const bool acc = processHit(s, o, d, h.id, P->hit_min_gaussian_response, P->alpha_min,
-                                                P->sph_eval_degree, st, &ev);
+                                                P->sph_eval_degree, st, &ev, out_margin ? &fc : nullptr);
                     if (g_trace)
                         g_trace->insert(g_trace->end(), {(float)h.id, h.t, ev.gres, ev.galpha, st.T, acc ? 1.0f : 0.0f,
                                                          (float)rounds});
                     if (out_margin) {
-                        m_thr = std::min(m_thr, std::fabs(ev.gres / P->hit_min_gaussian_response - 1.0f));
-                        m_thr = std::min(m_thr, std::fabs(ev.galpha / P->alpha_min - 1.0f));
-                        if (acc) m_thr = std::min(m_thr, std::fabs(st.T / P->min_transmittance - 1.0f));
+                        const float r0 = std::fabs(ev.gres / P->hit_min_gaussian_response - 1.0f);
+                        const float r1 = std::fabs(ev.galpha / P->alpha_min - 1.0f);
+                        m_thr = std::min(m_thr, std::min(r0, r1));
+                        if (r0 < FLAG_THR_EPS || r1 < FLAG_THR_EPS) flag(T_before * ev.galpha, h.id);
+                        if (acc) {
+                            const float r2 = std::fabs(st.T / P->min_transmittance - 1.0f);
+                            m_thr = std::min(m_thr, r2);
+                            if (r2 < FLAG_THR_EPS) {  // the ray may go on: the next crossing's colour
+                                const Hit nx = i + 1 < MAX_HIT_PER_TRACE ? kb[i + 1] : h_out;
+                                flag(st.T, nx.id);
+                            }
+                        }
                         // (an inclusive tmin re-finds the same crossing: not an ordering question)
                         const bool refound = h.id == prev_id && h.t == prev_t;
-                        if (acc && round_start && prev_t == prev_t && !refound) m_b = std::min(m_b, gap(h.t, prev_t));
-                        if (acc && prev_acc_t == prev_acc_t && !refound) m_t = std::min(m_t, gap(h.t, prev_acc_t));
+                        if (acc && round_start && prev_t == prev_t && !refound) {
+                            const float gg = gap(h.t, prev_t);
+                            m_b = std::min(m_b, gg);
+                            if (gg < FLAG_BOUND_EPS) flag(T_before * ev.galpha, h.id);
+                        }
+                        if (acc && prev_acc_t == prev_acc_t && !refound) {
+                            const float gg = gap(h.t, prev_acc_t);
+                            m_t = std::min(m_t, gg);
+                            if (gg < FLAG_PAIR_EPS) flag(prev_acc_T * prev_acc_a * ev.galpha, h.id);
+                        }
                         round_start = false;
                         prev_t = h.t;
                         prev_id = h.id;
-                        if (acc) prev_acc_t = h.t;
+                        if (acc) {
+                            prev_acc_t = h.t;
+                            prev_acc_T = T_before;
+                            prev_acc_a = ev.galpha;
+                        }
                         if (h.t > last) last_ids.clear();
                         if (h.t >= last) last_ids.push_back(h.id);
                         // the crossing that ends the ray against its successor: a tie decides which of
@@ -821,8 +895,12 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                         if (acc && !(st.T > P->min_transmittance)) {
                             const Hit nx = i + 1 < MAX_HIT_PER_TRACE && kb[i + 1].id != INVALID_PARTICLE_ID ? kb[i + 1]
                                                                                                           : h_out;
-                            if (nx.id != INVALID_PARTICLE_ID && gap(h.t, nx.t) < 1e-4f && accepted(nx.id))
-                                m_b = std::min(m_b, gap(h.t, nx.t));
+                            if (nx.id != INVALID_PARTICLE_ID && gap(h.t, nx.t) < 1e-4f && accepted(nx.id)) {
+                                const float gg = gap(h.t, nx.t);
+                                m_b = std::min(m_b, gg);
+                                if (gg < FLAG_BOUND_EPS)
+                                    flag(T_before * (ev.galpha + evalResponse(s, nx.id, o, d).galpha), nx.id);
+                            }
                         }
                     }
                     last = std::max(last, h.t);
@@ -840,9 +918,10 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
             out_stats[3 * oi + 2] = rounds;
         }
         if (out_margin) {
-            out_margin[3 * oi] = m_thr;
-            out_margin[3 * oi + 1] = m_t;
-            out_margin[3 * oi + 2] = m_b;
+            out_margin[4 * oi] = m_thr;
+            out_margin[4 * oi + 1] = m_t;
+            out_margin[4 * oi + 2] = m_b;
+            out_margin[4 * oi + 3] = flagged ? (fw + P->min_transmittance) * fc : 0.0f;
         }
     }
     return 0;

@@ -55,6 +55,8 @@ def lib():
         L.oracle_kernel_scale.argtypes = [C.c_float, C.c_float, C.c_uint32, C.c_float]
         L.oracle_kernel_scale.restype = C.c_float
         L.oracle_radiance_from_sh.argtypes = [C.c_uint32, vp, vp, vp]
+        L.oracle_flag_eps.argtypes = [vp]
+        L.oracle_flag_eps.restype = None
         _lib = L
     return _lib
 
@@ -119,7 +121,7 @@ def render(enc, view_inv, proj_inv, width, height, ncams=1, params=None, subset=
     rgba = np.zeros((nr, 4), np.float32)
     depth = np.zeros(nr, np.float32)
     stats = np.zeros((nr, 3), np.uint32)
-    margin = np.zeros((nr, 3), np.float32)
+    margin = np.zeros((nr, 4), np.float32)
     dirs = np.zeros((nr if subset is not None else width * height * ncams, 4), np.float32) if ray_dirs else None
     rc = lib().oracle_render(_p(enc["verts"]), _p(enc["tris"]), _p(enc["density"]), _p(enc["sh"]), enc["m"],
                              C.byref(p), _p(vi), _p(pi), width, height, ncams, _p(sub), 0 if sub is None else len(sub),
@@ -132,7 +134,7 @@ def render(enc, view_inv, proj_inv, width, height, ncams=1, params=None, subset=
         out["rgba32f"] = rgba.reshape(ncams, height, width, 4)
         out["stats"] = stats.reshape(ncams, height, width, 3)
         out["depth"] = depth.reshape(ncams, height, width)
-        out["margin"] = margin.reshape(ncams, height, width, 3)
+        out["margin"] = margin.reshape(ncams, height, width, 4)
     return out
 
 
@@ -186,7 +188,7 @@ class Scene:
         sub = None if subset is None else np.ascontiguousarray(subset, np.uint64)
         rgba = np.zeros((nr, 4), np.float32)
         stats = np.zeros((nr, 3), np.uint32)
-        marg = np.zeros((nr, 3), np.float32) if margin else None
+        marg = np.zeros((nr, 4), np.float32) if margin else None
         rc = lib().oracle_scene_render(self.h, C.byref(p), _p(vi), _p(pi), width, height, ncams, _p(sub),
                                        0 if sub is None else len(sub), _p(rgba), None, None, _p(stats), _p(marg),
                                        int(threads))
@@ -220,7 +222,30 @@ PAIR_EPS = 2e-6
 BOUND_EPS = 1e-5
 
 
+def _margin_rows(margin):
+    m = np.asarray(margin, np.float32)
+    cols = m.shape[-1] if m.ndim > 1 and m.shape[-1] in (3, 4) else 4
+    return m.reshape(-1, cols)
+
+
 def ambiguous(margin):
-    """Boolean mask of rays whose result legitimately depends on ulp-level float differences."""
-    m = np.asarray(margin, np.float32).reshape(-1, 3)
+    """Boolean mask of rays whose result legitimately depends on ulp-level float differences (margin columns
+    0..2; fixtures written before the flip bound have only those three)."""
+    m = _margin_rows(margin)
     return (m[:, 0] < THR_EPS) | (m[:, 1] < PAIR_EPS) | (m[:, 2] < BOUND_EPS)
+
+
+def flip_bound(margin):
+    """Per ray, the bound on |d rgb| that its flagged decisions allow (margin column 3, gvrt_oracle.cpp): the sum over
+    flagged decisions of T x alpha moved, plus minTransmittance, times the largest radiance channel on the ray."""
+    m = _margin_rows(margin)
+    if m.shape[1] < 4:
+        raise ValueError("margin without the flip-bound column (regenerate the fixture)")
+    return m[:, 3]
+
+
+def flag_eps():
+    """The C oracle's flag thresholds (must equal THR_EPS, PAIR_EPS, BOUND_EPS)."""
+    out = np.zeros(3, np.float32)
+    lib().oracle_flag_eps(_p(out))
+    return out

@@ -1,6 +1,9 @@
-"""Full-size SURVEY §8d configurations 3-5 on the GPU: size-independent properties plus an oracle
-check on a strided ray subset (the oracle restates the reference's loop per ray, so a subset is a
-valid sample).  Tolerances and the on-threshold accounting as in test_gpu_parity.py; tile / view splits are checked bit for bit.
+"""Full-size SURVEY §8d configurations 3-5 and the dense stand-in on the GPU: size-independent properties plus
+the oracle over the whole frame (garden) or a 1/64 strided ray sample (truck 4K: 130 k rays, the light field:
+518 k of its 33.2 M rays, the dense stand-in: 32 k rays, whose ~150 crossings per ray cost the oracle ~14 min
+of CPU per full frame).  The oracle restates the reference's loop per ray, so a strided sample is a valid
+sample.  Tolerances and the on-threshold accounting as in test_gpu_parity.py (every compared ray is bounded;
+on-threshold fractions capped near their measured values); tile / view splits are checked bit for bit.
 
   * config 3 "garden": 3 M Gaussians, 1920x1080
   * config 4 "truck":  2 M Gaussians, 3840x2160, image split in 64x64 blocks over 8 simulated ranks
@@ -9,7 +12,7 @@ valid sample).  Tolerances and the on-threshold accounting as in test_gpu_parity
 import numpy as np
 import pytest
 
-from test_gpu_parity import _cmp_images
+from test_gpu_parity import _cmp_images, parity_figures, record_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -19,14 +22,17 @@ def _scene(gv, name):
     return gv.scene.make(**gen), W, H, ncams
 
 
-def _oracle_subset(O, splats, vi, pi, W, H, ncams=1, stride=997):
+def _oracle_subset(O, splats, vi, pi, W, H, ncams=1, stride=1):
+    """The oracle on every stride-th ray of the frame(s) (stride 1: all of them)."""
     e = O.enclose(splats)
     sub = np.arange(0, W * H * ncams, stride, dtype=np.uint64)
     sc = O.Scene(e)
     try:
-        ref = sc.render(vi, pi, W, H, ncams=ncams, subset=sub, margin=True)
+        ref = sc.render(vi, pi, W, H, ncams=ncams, subset=None if stride == 1 else sub, margin=True)
     finally:
         sc.close()
+    if stride == 1:
+        ref = {k: v.reshape(len(sub), -1) for k, v in ref.items()}
     return e["m"], sub, ref
 
 
@@ -41,9 +47,11 @@ def test_garden_3m(gv, O):
     assert m > 2_700_000 and st["bvh_nodes"] > 0
     np.testing.assert_array_equal(a["rgba32f"], b["rgba32f"])  # deterministic
     assert (a["rgba32f"][..., 3] > 0).mean() > 0.5  # the object and the shell cover the frame
-    m_ref, sub, ref = _oracle_subset(O, splats, vi, pi, W, H)
+    m_ref, sub, ref = _oracle_subset(O, splats, vi, pi, W, H)  # all 2 073 600 rays
     assert m_ref == m
-    _cmp_images(a["rgba32f"].reshape(-1, 4)[sub.astype(np.int64)], ref)
+    got = a["rgba32f"].reshape(-1, 4)[sub.astype(np.int64)]
+    _cmp_images(got, ref, amb_max=0.015)
+    record_parity("garden", **parity_figures(O, gv, got, ref))
 
 
 def test_truck_4k_tile_split(gv, O):
@@ -65,8 +73,10 @@ def test_truck_4k_tile_split(gv, O):
         torch.cuda.synchronize()
     assert covered == ((W + 7) // 8) * ((H + 7) // 8)
     np.testing.assert_array_equal(frame.cpu().numpy(), full["rgba8"][0])
-    _, sub, ref = _oracle_subset(O, splats, vi, pi, W, H, stride=4001)
-    _cmp_images(full["rgba32f"].reshape(-1, 4)[sub.astype(np.int64)], ref)
+    _, sub, ref = _oracle_subset(O, splats, vi, pi, W, H, stride=64)
+    got = full["rgba32f"].reshape(-1, 4)[sub.astype(np.int64)]
+    _cmp_images(got, ref, amb_max=0.015)
+    record_parity("truck_4k", stride=64, **parity_figures(O, gv, got, ref))
 
 
 def test_lightfield_grid_16_views(gv, O):
@@ -86,8 +96,10 @@ def test_lightfield_grid_16_views(gv, O):
     np.testing.assert_allclose(np.linalg.norm(d[..., :3], axis=-1), 1.0, atol=2e-6)
     # neighbouring views see (slightly) different images
     assert np.abs(img[0] - img[15]).max() > 0.01
-    _, sub, ref = _oracle_subset(O, splats, vi, pi, W, H, ncams=ncams, stride=15013)
-    _cmp_images(img.reshape(-1, 4)[sub.astype(np.int64)], ref)
+    _, sub, ref = _oracle_subset(O, splats, vi, pi, W, H, ncams=ncams, stride=64)
+    got = img.reshape(-1, 4)[sub.astype(np.int64)]
+    _cmp_images(got, ref, amb_max=0.015)
+    record_parity("lightfield_16", stride=64, **parity_figures(O, gv, got, ref))
 
 
 def test_dense_standin(gv, O):
@@ -99,14 +111,16 @@ def test_dense_standin(gv, O):
         m = r.prepare(splats)
         fast = r.render(vi, pi, W, H, hit_counts=True)
         lit = r.render(vi, pi, W, H, mode=gv.MODE_LITERAL)
-    m_ref, sub, ref = _oracle_subset(O, splats, vi, pi, W, H, stride=2003)
+    m_ref, sub, ref = _oracle_subset(O, splats, vi, pi, W, H, stride=64)
     assert m_ref == m
     st = ref["stats"].reshape(-1, 3)
     assert st[:, 0].mean() > 140, st.mean(axis=0)  # the workload is what it claims to be
     idx = sub.astype(np.int64)
-    # ~150 crossings and ~10 round boundaries per ray: ~7 % of the rays carry a decision within the
-    # on-threshold margins (measured on this subset); every other ray must match as everywhere else
-    _cmp_images(fast["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.10)
-    _cmp_images(lit["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.10)
+    # ~150 crossings and ~10 round boundaries per ray: 7.3-7.4 % of the rays carry a decision within the
+    # on-threshold margins (measured on 1/32 and 1/64 samples); each of them is bounded by its flip bound,
+    # every other ray must match as everywhere else
+    _cmp_images(fast["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.08)
+    _cmp_images(lit["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.08)
     amb = O.ambiguous(ref["margin"])
     assert (fast["hit_counts"].reshape(-1)[idx] != st[:, 1])[~amb].sum() == 0
+    record_parity("dense", stride=64, **parity_figures(O, gv, fast["rgba32f"].reshape(-1, 4)[idx], ref))

@@ -3,16 +3,18 @@
 Tolerances (north star: "pixel-for-pixel within a stated float tolerance", PSNR >= 50 dB):
   * enclosing records: rtol 2e-6 / atol 1e-7 (expf / 1/sqrt ulps; FMA contraction on gfx950)
   * survivor count and compaction order: exact
-  * render, float RGBA vs the oracle with the same analytic proxy, per ray:
-      - rays "on a threshold" are accounted separately: the oracle reports, per ray, how close any of its
-        composite decisions came to a threshold (response vs hitMinGaussianResponse, alpha vs 1/255,
-        T vs minTransmittance: relative margin < 1e-4), how close two consecutive composited crossings
-        came in t (relative gap < 2e-6) and how close a crossing at a round / full-buffer / termination
-        boundary came to its neighbour (< 1e-5, or a bitwise tie dropped at the exclusive tmin, Q13),
-        see oracle.ambiguous.  Only these rays may legitimately decide differently under the GPU's
-        few-ulp exp / rsqrt / rcp; they must be rare (<= 2 %, ~1 % measured);
+  * render, float RGBA vs the oracle with the same analytic proxy, every compared ray:
+      - rays "on a threshold" (oracle.ambiguous): one of the ray's composite decisions came within a relative
+        1e-4 of a threshold (response vs hitMinGaussianResponse, alpha vs 1/255, T vs minTransmittance), two
+        consecutive composited crossings within 2e-6 in t, or a crossing at a round / full-buffer / termination
+        boundary within 1e-5 of its neighbour (or a bitwise tie dropped at the exclusive tmin, Q13).  Only these
+        rays may decide differently under the GPU's few-ulp exp / rsqrt / rcp.  Their fraction is capped per
+        configuration (default 2 %), and each of them is still bounded: |d rgb| <= the oracle's flip bound
+        (oracle.flip_bound: per flagged decision T x alpha moved x the largest radiance channel on the ray,
+        plus minTransmittance x that channel) + 1e-4;
       - every other ray: |d rgb| <= 1e-4 on >= 99.99 % of them, max |d rgb| <= 5e-3, and the accepted-hit
         count (alpha channel) equal;
+      - all compared rays together: rgba8 PSNR >= 50 dB.
   * render vs the literal restatement (20-triangle soup, watertight triangle test): PSNR >= 50 dB
 """
 import os
@@ -26,23 +28,36 @@ RTOL, ATOL = 2e-6, 1e-7
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def _cmp_images(a, ref, margin=None, frac_tol=1e-4, tol=1e-4, max_tol=5e-3, amb_max=0.02):
+def _cmp_images(a, ref, margin=None, frac_tol=1e-4, tol=1e-4, max_tol=5e-3, amb_max=0.02, psnr_min=50.0):
     """a: HIP rgba; ref: oracle output dict (rgba32f + margin) or a bare rgba array with `margin` given.
-    See the module docstring for the accounting."""
+    See the module docstring for the accounting; returns the number of on-threshold rays."""
     if isinstance(ref, dict):
         margin = ref["margin"] if margin is None else margin
         ref = ref["rgba32f"]
     import oracle as O
+    from importlib import import_module
+    gv = import_module("3dgvrt_lightfield_amd")
     a = np.asarray(a, np.float64).reshape(-1, 4)
     b = np.asarray(ref, np.float64).reshape(-1, 4)
     amb = O.ambiguous(margin) if margin is not None else np.zeros(len(a), bool)
     assert amb.sum() <= max(amb_max * amb.size, 3), f"{int(amb.sum())} of {amb.size} rays on a threshold"
-    d = np.abs(a[:, :3] - b[:, :3]).max(axis=1)[~amb]
+    dall = np.abs(a[:, :3] - b[:, :3]).max(axis=1)
+    d = dall[~amb]
     bad = (d > tol).mean() if d.size else 0.0
     assert bad <= frac_tol, f"{bad:.6f} of off-threshold rays differ by more than {tol} (max {d.max():.4g})"
     assert d.size == 0 or d.max() <= max_tol, f"max |d rgb| = {d.max():.4g} on an off-threshold ray"
     am = (a[:, 3] != b[:, 3])[~amb]
     assert am.sum() <= frac_tol * am.size, f"{int(am.sum())} off-threshold rays differ in accepted-hit count"
+    if amb.any():
+        # on-threshold rays: bounded by what their flagged decisions can move (fixtures written before the
+        # flip bound carry three margin columns: those rays are then bounded by the frame PSNR alone)
+        if np.asarray(margin).shape[-1] == 4:
+            fb = O.flip_bound(margin)[amb].astype(np.float64)
+            over = dall[amb] - (fb + tol)
+            assert (over <= 0).all(), (f"{int((over > 0).sum())} on-threshold rays beyond their flip bound: "
+                                       f"|d| {dall[amb][over > 0][:5]} bound {fb[over > 0][:5]}")
+    p = gv.psnr_rgb(gv.quantize_rgba8(a.astype(np.float32)), gv.quantize_rgba8(b.astype(np.float32)))
+    assert p >= psnr_min, f"rgba8 PSNR over all {len(a)} compared rays {p:.2f} dB"
     return int(amb.sum())
 
 
@@ -457,11 +472,37 @@ def bicycle(gv):
     return gv.scene.mipnerf_standin(1_000_000, seed=1)
 
 
-def test_bicycle_subset_vs_oracle_and_fast_literal(gv, O, bicycle):
+def record_parity(name, **kw):
+    """Per-configuration parity figures (on-threshold fraction, worst deviations) for DESIGN.md, written to
+    gpurun_out/parity/<name>.json (the GPU box merges gpurun_out back)."""
+    import json
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "parity")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, name + ".json"), "w") as f:
+        json.dump(kw, f, indent=1)
+
+
+def parity_figures(O, gv, got, ref):
+    g = np.asarray(got, np.float64).reshape(-1, 4)
+    b = np.asarray(ref["rgba32f"], np.float64).reshape(-1, 4)
+    amb = O.ambiguous(ref["margin"])
+    d = np.abs(g[:, :3] - b[:, :3]).max(axis=1)
+    fb = O.flip_bound(ref["margin"])
+    return {"rays": int(len(g)), "on_threshold": int(amb.sum()), "on_threshold_frac": float(amb.mean()),
+            "max_abs_off_threshold": float(d[~amb].max()) if (~amb).any() else 0.0,
+            "frac_beyond_1e-4_off_threshold": float((d[~amb] > 1e-4).mean()) if (~amb).any() else 0.0,
+            "max_abs_on_threshold": float(d[amb].max()) if amb.any() else 0.0,
+            "max_ratio_to_flip_bound": float((d[amb] / (fb[amb] + 1e-4)).max()) if amb.any() else 0.0,
+            "psnr_rgba8_db": float(gv.psnr_rgb(gv.quantize_rgba8(g.astype(np.float32)),
+                                                gv.quantize_rgba8(b.astype(np.float32))))}
+
+
+def test_bicycle_full_frame_vs_oracle_and_fast_literal(gv, O, bicycle):
+    """Config 2 (the bench workload): every one of the 2 073 600 rays of the 1080p frame against the oracle."""
     W, H = 1920, 1080
     vi, pi = gv.scene.mipnerf_camera(W, H)
     with gv.Renderer(0) as r:
-        m = r.prepare(bicycle)
+        m = r.prepare(bicycle, builder=2, collapse=1)  # the bench's quality build
         fast = r.render(vi, pi, W, H)
         lit = r.render(vi, pi, W, H, mode=gv.MODE_LITERAL)
         again = r.render(vi, pi, W, H)
@@ -472,11 +513,14 @@ def test_bicycle_subset_vs_oracle_and_fast_literal(gv, O, bicycle):
     # FAST == LITERAL on every ray but flagged ties / threshold rays (each differing ray re-marched)
     n = _fast_vs_literal(O, e, fast["rgba32f"], lit["rgba32f"], vi, pi, W, H)
     assert n <= 1e-4 * W * H, n
-    sub = np.arange(0, W * H, 997, dtype=np.uint64)  # ~2 k rays spread over the frame
-    ref = O.render(e, vi, pi, W, H, proxy_mode=1, subset=sub)
-    got = fast["rgba32f"].reshape(-1, 4)[sub.astype(np.int64)]
-    _cmp_images(got, ref)
-    assert gv.psnr_rgb(gv.quantize_rgba8(got), gv.quantize_rgba8(ref["rgba32f"])) >= 50.0
+    sc = O.Scene(e)
+    try:
+        ref = sc.render(vi, pi, W, H, margin=True)
+    finally:
+        sc.close()
+    _cmp_images(fast["rgba32f"], ref, amb_max=0.015)
+    _cmp_images(lit["rgba32f"], ref, amb_max=0.015)
+    record_parity("bicycle", **parity_figures(O, gv, fast["rgba32f"], ref), fast_literal_differ=n)
 
 
 def test_unpacked_fast_path_matches(gv, config1):

@@ -235,3 +235,29 @@ def test_camera_math(gv):
     # ndc y = -1 (image row 0) looks up (+y in camera space): Vulkan y-flip of the modified glm
     t = Pi @ np.array([0.0, -1.0, 1.0, 1.0])
     assert t[1] > 0
+
+
+def test_flag_thresholds_shared_with_the_c_oracle(O):
+    np.testing.assert_array_equal(O.flag_eps(), np.array([O.THR_EPS, O.PAIR_EPS, O.BOUND_EPS], np.float32))
+
+
+@pytest.mark.parametrize("kw", [{k: v * (1 + sgn * 9e-5)} for k, v in (("hit_min_gaussian_response", 0.0113),
+                                                                       ("alpha_min", 0.0039215686275),
+                                                                       ("min_transmittance", 0.001))
+                                for sgn in (1, -1)])
+def test_flip_bound_covers_threshold_perturbations(gv, O, config1, config1_enc, kw):
+    """The parity accounting's flip bound (margin column 3) is an actual bound: moving a threshold by a relative
+    9e-5 (inside the 1e-4 flag margin) changes only flagged rays, each by no more than its flip bound (measured:
+    at most 0.46 of it)."""
+    W = H = 256
+    vi, pi = gv.scene.config1_camera(W, H)
+    ref = O.render(config1_enc, vi, pi, W, H, proxy_mode=1)
+    per = O.render(config1_enc, vi, pi, W, H, proxy_mode=1, **kw)
+    d = np.abs(per["rgba32f"][..., :3] - ref["rgba32f"][..., :3]).max(axis=-1).reshape(-1)
+    amb = O.ambiguous(ref["margin"])
+    fb = O.flip_bound(ref["margin"])
+    changed = d > 1e-6
+    assert changed.any()                       # the perturbation does flip decisions
+    assert amb[changed].all()                  # only on flagged rays
+    assert (d[changed] <= fb[changed] + 1e-6).all(), (d[changed] / fb[changed]).max()
+    assert (fb[~amb] == 0).all() and (fb[amb] > 0).mean() > 0.5
