@@ -33,6 +33,23 @@ def rank_views(views, world):
     return [list(range(r, views, world)) for r in range(world)]
 
 
+def balanced_views(costs, world):
+    """Cost-weighted view assignment (config 5 on N ranks): every rank gets floor or ceil(views / world) views, and
+    the views are placed costliest first, each on the rank with the least cost so far among those with room
+    (longest-processing-time list scheduling with a count bound; ties by rank, then view index, so every rank
+    computes the same assignment from the same costs).  Views of a rank are returned in increasing index."""
+    costs = [float(c) for c in costs]
+    n = len(costs)
+    cap = [n // world + (1 if r < n % world else 0) for r in range(world)]
+    load = [0.0] * world
+    out = [[] for _ in range(world)]
+    for v in sorted(range(n), key=lambda i: (-costs[i], i)):
+        r = min((rr for rr in range(world) if len(out[rr]) < cap[rr]), key=lambda rr: (load[rr], rr))
+        out[r].append(v)
+        load[r] += costs[v]
+    return [sorted(g) for g in out]
+
+
 def unpack_tiles_host(packed, tiles, width, height, ncams=1, frame=None):
     """Host mirror of k_unpack (gvrt_render.hip): packed[i*64 + lane] -> frame[cam][ty*8 + lane//8][tx*8 + lane%8]."""
     packed = np.asarray(packed).reshape(-1, 64, packed.shape[-1] if packed.ndim > 1 else 1)

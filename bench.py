@@ -73,6 +73,9 @@ def parse():
     ap.add_argument("--rank-balance", type=int, default=0,
                     help="one GPU only: also time each of N ranks' parts of the split (tile lists of --split tiles, "
                          "view groups of --split views) as that rank would render it, and report the imbalance")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=0|1",
+                    help="per-handle tuning switch (gvrt_set_option; names in _lib.OPTIONS), for same-box A/B runs; "
+                         "none of them changes an image")
     ap.add_argument("--build", default="quality", choices=["quality", "fast"],
                     help="quality: device binned-SAH tree + SAH-optimal 4-wide collapse (the static-scene build, "
                          "as the reference's PREFER_FAST_TRACE BLAS); fast: device LBVH + greedy collapse")
@@ -125,6 +128,10 @@ def pmc_passes(args):
              "--no-cpu-baseline", "--no-stats", "--no-pmc"]
     if args.ply:
         child += ["--ply", args.ply]
+    for kv in args.option:
+        child += ["--option", kv]
+    if args.camera_path != "static":
+        child += ["--camera-path", args.camera_path, "--orbit-step", str(args.orbit_step)]
     out = {}
     passes = [["FETCH_SIZE"], ["WRITE_SIZE"], ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM"]]
     tmp = tempfile.mkdtemp(prefix="gvrt_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
@@ -156,7 +163,19 @@ def pmc_passes(args):
     return out
 
 
-def rank_balance(args, r, gv, dist_mod, vi_all, pi, W, H, views, params, full_ms, reps=4):
+def view_cost_calibration(r, vis, pi, W, H, params, reps=2):
+    """Kernel ms of each view of the rig rendered alone (the last of `reps` launches: cost-ordered)."""
+    import torch
+    buf = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+    out = []
+    for v in np.asarray(vis, np.float32).reshape(-1, 16):
+        for _ in range(reps):
+            r.render_device(np.ascontiguousarray(v), pi, W, H, 1, params=params, rgba8_ptr=buf.data_ptr())
+        out.append(float(r.render_ms()))
+    return out
+
+
+def rank_balance(args, r, gv, dist_mod, vi_all, pi, W, H, views, params, full_ms, reps=4, view_costs=None):
     """Strong-scaling imbalance measured on one GPU: each of N ranks' parts of the split rendered alone, as that
     rank renders it (its own cost-ordered dispatch: the part is rendered `reps` times, the first launch of a
     list being unordered, and the later ones' median kept).  Tile split: the 64x64-block round-robin tile
@@ -177,8 +196,9 @@ def rank_balance(args, r, gv, dist_mod, vi_all, pi, W, H, views, params, full_ms
             ms.append(float(np.median(got[1:])))
         what = f"{n} tile lists (64x64-pixel blocks round-robin), {parts[0].shape[0]}..{parts[-1].shape[0]} tiles each"
     else:
-        groups = dist_mod.rank_views(views, n)
         vis = np.asarray(vi_all, np.float32).reshape(-1, 16)
+        rr = dist_mod.rank_views(views, n)
+        groups = dist_mod.balanced_views(view_costs, n) if view_costs else rr
         buf = torch.zeros((max(len(g) for g in groups), H, W, 4), dtype=torch.uint8, device=dev)
         for g in groups:
             if not g:
@@ -189,9 +209,18 @@ def rank_balance(args, r, gv, dist_mod, vi_all, pi, W, H, views, params, full_ms
                                 rgba8_ptr=buf.data_ptr())
                 got.append(r.render_ms())
             ms.append(float(np.median(got[1:])))
-        what = f"{n} view groups of the {views}-view rig ({len(groups[0])} views each)"
+        what = (f"{n} view groups of the {views}-view rig ({len(groups[0])} views each), "
+                + ("cost-balanced (dist.balanced_views: " + str(groups) + ")" if view_costs else "round-robin"))
     mean, mx = float(np.mean(ms)), float(np.max(ms))
-    return {"ranks": n, "parts": what, "kernel_ms": [round(x, 4) for x in ms], "max_over_mean": round(mx / mean, 4),
+    extra = {}
+    if args.split != "tiles" and view_costs:
+        # the round-robin assignment the balancing replaces, from the same per-view costs
+        rrc = [sum(view_costs[v] for v in g) for g in dist_mod.rank_views(views, n)]
+        bc = [sum(view_costs[v] for v in g) for g in groups]
+        extra = {"view_ms": [round(x, 4) for x in view_costs],
+                 "round_robin_max_over_mean_est": round(max(rrc) / float(np.mean(rrc)), 4),
+                 "balanced_max_over_mean_est": round(max(bc) / float(np.mean(bc)), 4)}
+    return {**extra, "ranks": n, "parts": what, "kernel_ms": [round(x, 4) for x in ms], "max_over_mean": round(mx / mean, 4),
             "full_kernel_ms": round(full_ms, 4), "implied_efficiency": round(full_ms / (n * mx), 4),
             "note": "each part alone on one GPU with its own cost-ordered dispatch; median of the ordered launches"}
 
@@ -234,6 +263,9 @@ def main():
     n_input = splats["positions"].size // 3
 
     r = gv.Renderer(local_rank)
+    for kv in args.option:
+        name, _, val = kv.partition("=")
+        r.set_option(name, int(val))
     bkw = dict(builder=2, collapse=1) if args.build == "quality" else {}
     m = r.prepare(splats, **bkw)
     first_build = r.stats()  # includes the one-time lazy loading of the build kernels' code objects
@@ -262,8 +294,19 @@ def main():
     vis, pi = rigs[0]
     mode = gv.MODE_FAST if args.mode == "fast" else gv.MODE_LITERAL
     params = r.render_params(mode=mode)
+    view_costs = None
     if args.split == "views":
         all_views = dist_mod.rank_views(views, world)
+        if views > world:
+            # more views than ranks (config 5): views differ in cost (measured up to 1.4x), so they are assigned by
+            # cost: rank 0 times each view alone once (its second launch, cost-ordered), every rank gets the costs
+            # (one broadcast at set-up, not per frame) and computes the same assignment (dist.balanced_views)
+            view_costs = view_cost_calibration(r, rigs[0][0], rigs[0][1], W, H, params) if rank == 0 else [0.0] * views
+            if distributed:
+                t = torch.tensor(view_costs, dtype=torch.float64, device=dev)
+                dist.broadcast(t, src=0)
+                view_costs = t.cpu().tolist()
+            all_views = dist_mod.balanced_views(view_costs, world)
         my_views = all_views[rank]
         frame_vi = [np.ascontiguousarray(v[my_views].reshape(-1)) for v, _ in rigs]
         ncams = len(my_views)
@@ -371,14 +414,18 @@ def main():
     digest = None
     if rank == 0:
         if distributed:
-            img = full if packed else ex.recv[(ex.frames - 1) % ex.nbuf][0][0]
+            if packed:
+                img = full
+            else:  # view 0 in the part of the rank that rendered it
+                r0 = next(k for k, g in enumerate(all_views) if 0 in g)
+                img = ex.recv[(ex.frames - 1) % ex.nbuf][r0][all_views[r0].index(0)]
         else:
             img = frame if not packed else None
             if packed:  # one rank: unpack the whole frame's tiles
                 img = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
                 r.unpack_tiles_rgba8(frame.data_ptr(), tiles, W, H, img.data_ptr())
             else:
-                img = frame[0]
+                img = frame[my_views.index(0)]
         torch.cuda.synchronize()
         digest = hashlib.sha1(img.cpu().numpy().tobytes()).hexdigest()
 
@@ -462,8 +509,13 @@ def main():
                              "frac_beyond_1e-4_off_threshold": float((d[~amb] > 1e-4).mean()) if (~amb).any() else 0.0,
                              "frac_beyond_1e-4_all": float((d > 1e-4).mean())}
 
-        balance = rank_balance(args, r, gv, dist_mod, frame_vi[0], pi, W, H, views, params, kern_avg) \
-            if args.rank_balance > 1 and world == 1 else None
+        balance = None
+        if args.rank_balance > 1 and world == 1:
+            if args.split == "views" and views > args.rank_balance:
+                vc = view_cost_calibration(r, rigs[0][0], rigs[0][1], W, H, params)
+            else:
+                vc = None
+            balance = rank_balance(args, r, gv, dist_mod, frame_vi[0], pi, W, H, views, params, kern_avg, view_costs=vc)
 
         result = {
             "metric": "Mrays/s + fps @1920x1080, 1M Gaussians; PSNR vs Vulkan reference",
@@ -474,7 +526,9 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak" if args.split == "views" else "strong",
+            # weak: each rank's work is fixed as N grows (one view per rank); strong: the total is fixed (one frame
+            # tile-split, or the 16-view light field over N <= 16 ranks)
+            "scaling": "weak" if args.split == "views" and views == world else "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": (f"real scene {os.path.basename(args.ply)}" if args.ply
@@ -494,6 +548,7 @@ def main():
             "kernel_mrays": round(rays_per_rank / (kern_avg * 1e-3) / 1e6, 3) if kern_avg == kern_avg else None,
             "psnr_vs_oracle_db": None if psnr is None else (round(psnr, 2) if math.isfinite(psnr) else "inf"),
             "frame_sha1": digest,
+            "options": {kv.partition("=")[0]: int(kv.partition("=")[2]) for kv in args.option} or None,
             "camera_path": (f"orbit: azimuth 30 + {args.orbit_step} deg per frame (every frame a new camera; the "
                             f"cost order of each frame from its predecessor)" if args.camera_path == "orbit"
                             else "static: every frame the config camera"),

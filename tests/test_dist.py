@@ -176,3 +176,21 @@ def test_launch_ranks_gives_n_processes():
     r = subprocess.run([sys.executable, probe, "--gpus", "2"], capture_output=True, text=True, timeout=120,
                        env=dict(env, WORLD_SIZE="3", RANK="0"))
     assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
+
+
+def test_balanced_views_equal_counts_and_lpt(gv):
+    """dist.balanced_views: equal view counts per rank (floor / ceil), costliest views placed first on the least
+    loaded rank with room, deterministic; never worse than round-robin on skewed costs."""
+    from importlib import import_module
+    d = import_module("3dgvrt_lightfield_amd.dist")
+    rng = np.random.default_rng(3)
+    for views, world in ((16, 8), (16, 4), (5, 3), (7, 7), (9, 2)):
+        c = rng.uniform(1.0, 2.5, views)
+        g = d.balanced_views(c, world)
+        assert sorted(v for x in g for v in x) == list(range(views))
+        assert sorted(len(x) for x in g) == sorted(views // world + (1 if r < views % world else 0) for r in range(world))
+        assert g == d.balanced_views(list(c), world)
+        bal = max(sum(c[v] for v in x) for x in g)
+        rr = max(sum(c[v] for v in x) for x in d.rank_views(views, world))
+        assert bal <= rr + 1e-12
+    assert d.balanced_views([3.0, 1.0, 2.0, 2.0], 2) == [[0, 1], [2, 3]]
