@@ -8,8 +8,13 @@
 //   gvrt_app lightfield --ply P [--width 180 --height 180] --out D          (computeGaussianLightField)
 //   gvrt_app hitcounts  --ply P [...] --out D                                (printRayHitCounts)
 //   gvrt_app bench      --ply P [--duration 10 --warmup 1 --frametimes] --out D   (vks::Benchmark, fps.txt)
+//   gvrt_app split      --ply P --rank R --world N --id-file F [--frames K] --out D
+//                       (one process per GPU: this rank's tiles of each frame, RCCL gather to rank 0, gvrt_rccl.h;
+//                        rank 0 writes split_frame.png, checks it against a one-GPU render of the same frame and
+//                        prints one JSON line)
 //   gvrt_app cameras    [--width W --height H] [--transforms T]   (prints the camera matrices; no GPU)
 //   gvrt_app png        OUT.png                                   (writes a test pattern; no GPU)
+//   gvrt_app tiles      --rank R --world N [--width W --height H]  (this rank's split tile list; no GPU)
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -20,6 +25,12 @@
 #include <sys/stat.h>
 
 #include "gvrt_host.h"
+#include "gvrt_rccl.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <chrono>
+#include <vector>
 
 using gvrt_host::GvrtApp;
 using gvrt_host::preset_camera;
@@ -72,10 +83,10 @@ gm::vec3 parse_vec3(const std::string& s) {
 
 int usage() {
     std::fprintf(stderr,
-                 "usage: gvrt_app {render|eval|lightfield|hitcounts|bench|cameras|png} [--ply P] [--out D]\n"
+                 "usage: gvrt_app {render|eval|lightfield|hitcounts|bench|split|cameras|png} [--ply P] [--out D]\n"
                  "       [--width W] [--height H] [--camera orbit|config1] [--variant rq|rt] [--transforms T]\n"
                  "       [--duration S] [--warmup S] [--frametimes] [--split-cells N] [--build fast|quality]\n"
-                 "       [--device I]\n");
+                 "       [--device I] [--rank R --world N --id-file F --frames K]\n");
     return 2;
 }
 
@@ -99,6 +110,12 @@ int main(int argc, char** argv) {
                     p[3] = (uint8_t)(255 - ((x + y) & 0x7F));
                 }
             return write_png(out, img.data(), W, H) ? 0 : 1;
+        }
+        if (a.cmd == "tiles") {  // host-only: the tile split of gvrt_rccl.h, "tx ty cam" per line
+            for (const gvrt_tile& t : gvrt_host::rank_tiles(W, H, 1, std::atoi(a.get("rank", "0").c_str()),
+                                                             std::atoi(a.get("world", "1").c_str())))
+                std::printf("%u %u %u\n", t.tx, t.ty, t.cam);
+            return 0;
         }
         if (a.cmd == "cameras") {  // host-only: the camera matrices the C-ABI receives (uint32 bit patterns)
             for (const char* n : {"config1", "orbit"}) {
@@ -172,6 +189,39 @@ int main(int argc, char** argv) {
         } else if (a.cmd == "hitcounts") {
             app.printRayHitCounts(cam, W, H, out + "/rayHitCountsOutput.txt");
             std::printf("wrote %s/rayHitCountsOutput.txt\n", out.c_str());
+        } else if (a.cmd == "split") {
+            const int rank = std::atoi(a.get("rank", "0").c_str()), world = std::atoi(a.get("world", "1").c_str());
+            const int frames = std::atoi(a.get("frames", "10").c_str());
+            ncclUniqueId id;
+            std::string err;
+            if (gvrt_host::rccl_rendezvous(a.get("id-file", out + "/rccl.id"), rank, &id, &err) != GVRT_OK)
+                throw std::runtime_error(err);
+            app.updateUniformBuffer(cam);
+            void* frame = nullptr;
+            if (rank == 0 && hipMalloc(&frame, (size_t)4 * W * H) != hipSuccess) throw std::runtime_error("frame alloc");
+            std::vector<uint8_t> got((size_t)4 * W * H), one((size_t)4 * W * H);
+            double ms = 0.0;
+            {
+                gvrt_host::SplitFrame sf(app, rank, world, id, W, H);
+                if (sf.status() != GVRT_OK) throw std::runtime_error("SplitFrame: " + sf.error());
+                if (sf.draw(frame) != GVRT_OK || sf.sync() != GVRT_OK) throw std::runtime_error(sf.error());  // warm-up
+                const auto t0 = std::chrono::steady_clock::now();
+                for (int k = 0; k < frames; ++k)
+                    if (sf.draw(frame) != GVRT_OK) throw std::runtime_error(sf.error());
+                if (sf.sync() != GVRT_OK) throw std::runtime_error(sf.error());
+                ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / frames;
+                if (rank == 0 && hipMemcpy(got.data(), frame, got.size(), hipMemcpyDeviceToHost) != hipSuccess)
+                    throw std::runtime_error("frame readback");
+            }
+            if (rank == 0) {
+                (void)hipFree(frame);
+                app.draw(cam, W, H, one.data());  // the same frame on this GPU alone
+                const bool same = got == one;
+                if (!write_png(out + "/split_frame.png", got.data(), W, H)) throw std::runtime_error("cannot write png");
+                std::printf("{\"world\": %d, \"frames\": %d, \"ms_per_frame\": %.4f, \"identical_to_one_gpu\": %s}\n",
+                            world, frames, ms, same ? "true" : "false");
+                if (!same) return 3;
+            }
         } else if (a.cmd == "bench") {  // vks::Benchmark (seconds are whole, as benchmark.hpp's uint32_t)
             vks::Benchmark& b = app.benchmark;
             b.duration = (uint32_t)std::atoi(a.get("duration", "10").c_str());

@@ -1,0 +1,73 @@
+// gvrt_rccl.h — the multi-GPU frame split of the C++ host over RCCL (north_star: "the image is
+// optionally tile-partitioned across 8 GPUs with RCCL gather over xGMI").
+//
+// One process per GPU.  Every rank holds the whole scene (GvrtApp::prepare; the build is deterministic, so the
+// ranks' BVHs are identical) and renders its own tiles of each frame: 64x64-pixel blocks dealt round-robin over
+// the ranks (rank_tiles, the same lists as the Python layer's dist.rank_tiles), tile-packed.  One exchange per
+// frame: grouped ncclSend / ncclRecv of the packed parts to rank 0 (rank 0 sends its own part to itself, so a
+// one-rank communicator runs the same path), then rank 0 scatters each part into the frame with
+// gvrt_unpack_tiles_rgba8.  The render, the exchange and the scatter are queued on one HIP stream (the handle
+// renders on it, gvrt_set_stream), so a frame costs no host round trip.  The reference has no multi-GPU path:
+// this replaces the single vkCmdTraceRaysKHR of buildCommandBuffer (VulkanFullRT.cpp:1217-1230) by N of them.
+//
+// Errors are statuses: an RCCL failure is GVRT_ERR_RCCL (include/gvrt.h), a HIP failure GVRT_ERR_HIP; error()
+// has the text.
+#pragma once
+#include <rccl/rccl.h>
+
+#include <string>
+#include <vector>
+
+#include "gvrt_host.h"
+
+namespace gvrt_host {
+
+// this rank's 8x8 tiles: (block*8)^2-pixel blocks round-robin over `world` ranks, per camera (dist.rank_tiles)
+std::vector<gvrt_tile> rank_tiles(uint32_t width, uint32_t height, uint32_t ncams, int rank, int world,
+                                  uint32_t block = 8);
+
+// Rendezvous of the communicator: rank 0 creates the RCCL unique id and writes it to `path` (written to a
+// temporary name and renamed, so a reader never sees half a file); every other rank waits for the file (up to
+// timeout_s seconds).  Returns GVRT_OK or GVRT_ERR_RCCL / GVRT_ERR_IO with the text in *err.
+gvrt_status rccl_rendezvous(const std::string& path, int rank, ncclUniqueId* id, std::string* err,
+                            double timeout_s = 120.0);
+
+class SplitFrame {
+  public:
+    // ncclCommInitRank(world, id, rank) on the app's device; the app's handle then renders on this object's stream
+    SplitFrame(GvrtApp& app, int rank, int world, const ncclUniqueId& id, uint32_t width, uint32_t height);
+    ~SplitFrame();
+    SplitFrame(const SplitFrame&) = delete;
+    SplitFrame& operator=(const SplitFrame&) = delete;
+
+    gvrt_status status() const { return st_; }  // of the constructor (communicator, buffers)
+    const std::string& error() const { return err_; }
+
+    // one frame with the app's uniformDataDynamic: this rank's tiles rendered tile-packed, gathered to rank 0 and
+    // scattered into `frame` (device rgba8 [H][W][4], rank 0 only; ignored elsewhere).  Queued on the stream.
+    gvrt_status draw(void* frame);
+    gvrt_status sync();  // waits for every queued frame on this rank
+
+    int rank() const { return rank_; }
+    int world() const { return world_; }
+    const std::vector<gvrt_tile>& tiles() const { return tiles_; }
+    double lastKernelMs() const;  // mean kernel time of the frames completed by the last sync (gvrt_stats)
+
+  private:
+    gvrt_status fail(gvrt_status s, const std::string& m);
+    gvrt_status rccl(ncclResult_t r, const char* what);
+
+    GvrtApp& app_;
+    int rank_, world_;
+    uint32_t width_, height_;
+    gvrt_status st_ = GVRT_OK;
+    std::string err_;
+    ncclComm_t comm_ = nullptr;
+    hipStream_t stream_ = nullptr;
+    std::vector<gvrt_tile> tiles_;                  // this rank's tile list
+    std::vector<std::vector<gvrt_tile>> all_tiles_;  // every rank's (rank 0 scatters with them)
+    void* d_part_ = nullptr;                         // this rank's packed part: tiles * 64 px * 4 B
+    std::vector<void*> d_recv_;                      // rank 0: one receive buffer per rank
+};
+
+}  // namespace gvrt_host

@@ -114,3 +114,26 @@ def test_cpp_app_flows_match_python(gv, tmp_path):
                 "--out", str(out))
     assert "Benchmark finished" in s and "fps    : " in s
     assert (out / "fps.txt").read_text().startswith("device,driverversion,duration (ms),frames,fps\n")
+
+
+def test_cpp_rccl_split_frame_one_rank(gv, tmp_path):
+    """The native multi-GPU path of the C++ host (host/gvrt_rccl.h SplitFrame: ncclCommInitRank, this rank's
+    tiles rendered tile-packed, grouped ncclSend / ncclRecv to rank 0, gvrt_unpack_tiles_rgba8) with a one-rank
+    communicator: rank 0 sends its part to itself through RCCL, and the gathered frame equals the one-GPU frame
+    byte for byte (the app checks and prints it)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "3dgvrt_lightfield_amd", "gvrt_app")
+    ply = str(tmp_path / "scene.ply")
+    gv.save_ply(ply, gv.scene.config1(n=3000))
+    import subprocess
+    for W, H in ((256, 256), (200, 120)):
+        r = subprocess.run([exe, "split", "--ply", ply, "--rank", "0", "--world", "1", "--id-file",
+                            str(tmp_path / f"rccl_{W}.id"), "--frames", "4", "--camera", "config1", "--width", str(W),
+                            "--height", str(H), "--out", str(tmp_path / f"split_{W}")],
+                           capture_output=True, text=True, timeout=180,
+                           env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+        assert r.returncode == 0, r.stderr[-2000:]
+        line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+        import json
+        d = json.loads(line)
+        assert d["identical_to_one_gpu"] is True and d["world"] == 1 and d["ms_per_frame"] > 0

@@ -191,3 +191,18 @@ def test_benchmark_fps_txt_matches_reference(tmp_path):
         assert outs[0][0] == outs[1][0], (outs[0][0][:300], outs[1][0][:300])
         assert outs[0][1] == outs[1][1], (outs[0][1], outs[1][1])
         assert outs[0][0].startswith(b"device,driverversion,duration (ms),frames,fps\n" + dev.encode() + b"," + drv.encode())
+
+
+@pytest.mark.parametrize("W,H,world", [(3840, 2160, 8), (1920, 1080, 3), (100, 60, 2), (8, 8, 4)])
+def test_cpp_split_tiles_match_python(gv, W, H, world):
+    """The C++ host's tile split (gvrt_rccl.h rank_tiles, the native RCCL path) deals the same 64x64-pixel blocks
+    to the same ranks as the Python layer (renderer.tiles_for_rank / dist.rank_tiles), and covers every tile
+    once."""
+    seen = []
+    for rank in range(world):
+        out = run("tiles", "--rank", str(rank), "--world", str(world), "--width", str(W), "--height", str(H))
+        got = np.array([[int(v) for v in l.split()] for l in out.splitlines()], np.int64).reshape(-1, 3)
+        ref = gv.tiles_for_rank(W, H, 1, rank, world, block=8).astype(np.int64)[:, :3]
+        np.testing.assert_array_equal(got, ref)
+        seen.extend(map(tuple, got))
+    assert len(seen) == len(set(seen)) == ((W + 7) // 8) * ((H + 7) // 8)
