@@ -706,8 +706,9 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                         bal2[k] = __builtin_amdgcn_ballot_w64(h2);
                     }
                 }
+                // children some lane hits without the cap (those no lane descends into are deferred, below)
 #pragma unroll
-                for (int k = 0; k < BVH_W; ++k) dm |= nz_bit(bal2[k] & ~bal[k], 1u << k);
+                for (int k = 0; k < BVH_W; ++k) dm |= nz_bit(bal2[k], 1u << k);
             } else if (octw) {
                 // (an opaque copy of 1/d: otherwise the first child's plane FMAs, common to both tests, are hoisted
                 // above the branch and every min / max input after it gets a canonicalising v_max)
@@ -739,6 +740,7 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
             leafmask = hm & ~inner;
             uint32_t im = hm & inner;
             if constexpr (FRONT) {
+                dm &= ~hm;  // deferred: hit by some lane without its cap, descended into by none
                 dleaf = dm & ~inner;
                 const uint32_t dmi = dm & inner;
                 uint32_t cm = im | dmi;

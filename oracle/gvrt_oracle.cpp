@@ -595,12 +595,14 @@ static thread_local std::vector<float>* g_trace = nullptr;
 //       whose crossings would be accepted (relative chord |tout - tin| / |t|), and 0 for a crossing
 //       dropped because its t tied bitwise with `last` (the exclusive-tmin round boundary, Q13);
 //   [3] flip bound: an upper bound on |d rgb| that the decisions flagged by [0..2] (below FLAG_*_EPS) can cause
-//       if a different float evaluation takes them the other way.  Each flagged decision moves the colour by at
-//       most (transmittance before it) x (opacity it moves) x (largest radiance channel involved): a threshold
-//       flip T_i a_i c, a swapped pair T_i a_i a_j |c_i - c_j|, a tie at a round / buffer / termination boundary
-//       T a c; the sum over the ray's flagged decisions, plus minTransmittance x c for the termination point the
-//       flip may move, with c the largest radiance channel of every crossing composited or flagged on the ray.
-//       0 for a ray with no flagged decision.
+//       if a different float evaluation takes them the other way.  Every flagged decision can at worst add or drop
+//       one crossing j (a threshold flip; a pair within PAIR_EPS that ties bitwise and straddles a round boundary
+//       of the other evaluation, where the exclusive tmin drops one of the two, Q13; a boundary tie), which moves
+//       the colour by at most 2 T_j a_j c (its own term, and the rescaling of everything behind it) plus the
+//       crossings a moved termination point adds or removes, at most minTransmittance / (1 - a_j) x c.  The bound is
+//       the sum over the ray's flagged crossings (both of a flagged pair) of 2 T_j a_j, plus minTransmittance / (1 -
+//       the largest such a_j), times c, the largest radiance channel of every crossing composited or flagged on the
+//       ray.  0 for a ray with no flagged decision.
 struct OracleScene {
     Scene s;
     Bvh bvh;
@@ -711,11 +713,14 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
         float m_thr = INFINITY, m_t = INFINITY, m_b = INFINITY, prev_t = NAN, prev_acc_t = NAN;
         // flip bound (out_margin[3]): summed T x alpha of the flagged decisions, the largest radiance channel
         // involved, and the previous accepted crossing's T before it and alpha (pair swaps)
-        float fw = 0.0f, fc = 0.0f, prev_acc_T = 0.0f, prev_acc_a = 0.0f;
+        float fw = 0.0f, fc = 0.0f, famax = 0.0f, prev_acc_T = 0.0f, prev_acc_a = 0.0f;
         bool flagged = false;
-        auto flag = [&](float w, uint32_t id) {
+        uint32_t prev_id_acc = INVALID_PARTICLE_ID;
+        // a crossing `id` that a flagged decision may add or drop, with T before it and its alpha
+        auto flag = [&](float T, float alpha, uint32_t id) {
             flagged = true;
-            fw += w;
+            fw += 2.0f * T * alpha;
+            famax = std::max(famax, alpha);
             if (id != INVALID_PARTICLE_ID) fc = std::max(fc, radianceMax(s, id, d, P->sph_eval_degree));
         };
         bool round_start = false;
@@ -739,7 +744,7 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                         m_b = 0.0f;  // dropped only because its t ties with the last processed crossing
                         const HitEval he = evalResponse(s, pid, o, d);
                         if (he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min)
-                            flag(T_round * he.galpha, pid);
+                            flag(T_round, he.galpha, pid);
                     }
                     return;
                 }
@@ -793,7 +798,10 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                             if (he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min) {
                                 const float gg = std::fabs(tout - tin) / std::max(std::fabs(tin), 1e-30f);
                                 m_b = std::min(m_b, gg);
-                                if (gg < FLAG_BOUND_EPS) flag(2.0f * T_round * he.galpha, g);
+                                if (gg < FLAG_BOUND_EPS) {  // both crossings of the proxy
+                                    flag(T_round, he.galpha, g);
+                                    flag(T_round, he.galpha, g);
+                                }
                             }
                         }
                         if (crossed) {
@@ -837,9 +845,9 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                 const float gg = gap(kb[MAX_HIT_PER_TRACE - 1].t, h_out.t);
                 m_b = std::min(m_b, gg);
                 if (gg < FLAG_BOUND_EPS) {
-                    flag(T_round * evalResponse(s, kb[MAX_HIT_PER_TRACE - 1].id, o, d).galpha,
+                    flag(T_round, evalResponse(s, kb[MAX_HIT_PER_TRACE - 1].id, o, d).galpha,
                          kb[MAX_HIT_PER_TRACE - 1].id);
-                    flag(T_round * evalResponse(s, h_out.id, o, d).galpha, h_out.id);
+                    flag(T_round, evalResponse(s, h_out.id, o, d).galpha, h_out.id);
                 }
             }
             round_start = true;
@@ -858,13 +866,14 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                         const float r0 = std::fabs(ev.gres / P->hit_min_gaussian_response - 1.0f);
                         const float r1 = std::fabs(ev.galpha / P->alpha_min - 1.0f);
                         m_thr = std::min(m_thr, std::min(r0, r1));
-                        if (r0 < FLAG_THR_EPS || r1 < FLAG_THR_EPS) flag(T_before * ev.galpha, h.id);
+                        if (r0 < FLAG_THR_EPS || r1 < FLAG_THR_EPS) flag(T_before, ev.galpha, h.id);
                         if (acc) {
                             const float r2 = std::fabs(st.T / P->min_transmittance - 1.0f);
                             m_thr = std::min(m_thr, r2);
-                            if (r2 < FLAG_THR_EPS) {  // the ray may go on: the next crossing's colour
+                            if (r2 < FLAG_THR_EPS) {  // the ray may go on (or stop before this crossing)
                                 const Hit nx = i + 1 < MAX_HIT_PER_TRACE ? kb[i + 1] : h_out;
-                                flag(st.T, nx.id);
+                                flag(T_before, ev.galpha, h.id);
+                                flag(st.T, 1.0f, nx.id);
                             }
                         }
                         // (an inclusive tmin re-finds the same crossing: not an ordering question)
@@ -872,12 +881,15 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                         if (acc && round_start && prev_t == prev_t && !refound) {
                             const float gg = gap(h.t, prev_t);
                             m_b = std::min(m_b, gg);
-                            if (gg < FLAG_BOUND_EPS) flag(T_before * ev.galpha, h.id);
+                            if (gg < FLAG_BOUND_EPS) flag(T_before, ev.galpha, h.id);
                         }
                         if (acc && prev_acc_t == prev_acc_t && !refound) {
                             const float gg = gap(h.t, prev_acc_t);
                             m_t = std::min(m_t, gg);
-                            if (gg < FLAG_PAIR_EPS) flag(prev_acc_T * prev_acc_a * ev.galpha, h.id);
+                            if (gg < FLAG_PAIR_EPS) {  // may swap, or tie and lose one at a round boundary
+                                flag(prev_acc_T, prev_acc_a, prev_id_acc);
+                                flag(T_before, ev.galpha, h.id);
+                            }
                         }
                         round_start = false;
                         prev_t = h.t;
@@ -886,6 +898,7 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                             prev_acc_t = h.t;
                             prev_acc_T = T_before;
                             prev_acc_a = ev.galpha;
+                            prev_id_acc = h.id;
                         }
                         if (h.t > last) last_ids.clear();
                         if (h.t >= last) last_ids.push_back(h.id);
@@ -898,8 +911,10 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                             if (nx.id != INVALID_PARTICLE_ID && gap(h.t, nx.t) < 1e-4f && accepted(nx.id)) {
                                 const float gg = gap(h.t, nx.t);
                                 m_b = std::min(m_b, gg);
-                                if (gg < FLAG_BOUND_EPS)
-                                    flag(T_before * (ev.galpha + evalResponse(s, nx.id, o, d).galpha), nx.id);
+                                if (gg < FLAG_BOUND_EPS) {
+                                    flag(T_before, ev.galpha, h.id);
+                                    flag(T_before, evalResponse(s, nx.id, o, d).galpha, nx.id);
+                                }
                             }
                         }
                     }
@@ -921,7 +936,8 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
             out_margin[4 * oi] = m_thr;
             out_margin[4 * oi + 1] = m_t;
             out_margin[4 * oi + 2] = m_b;
-            out_margin[4 * oi + 3] = flagged ? (fw + P->min_transmittance) * fc : 0.0f;
+            out_margin[4 * oi + 3] =
+                flagged ? (fw + P->min_transmittance / std::max(1.0f - famax, 0.01f)) * fc : 0.0f;
         }
     }
     return 0;

@@ -55,7 +55,8 @@ def _cmp_images(a, ref, margin=None, frac_tol=1e-4, tol=1e-4, max_tol=5e-3, amb_
             fb = O.flip_bound(margin)[amb].astype(np.float64)
             over = dall[amb] - (fb + tol)
             assert (over <= 0).all(), (f"{int((over > 0).sum())} on-threshold rays beyond their flip bound: "
-                                       f"|d| {dall[amb][over > 0][:5]} bound {fb[over > 0][:5]}")
+                                       f"rays {np.nonzero(amb)[0][over > 0][:5]} |d| {dall[amb][over > 0][:5]} "
+                                       f"bound {fb[over > 0][:5]}")
     p = gv.psnr_rgb(gv.quantize_rgba8(a.astype(np.float32)), gv.quantize_rgba8(b.astype(np.float32)))
     assert p >= psnr_min, f"rgba8 PSNR over all {len(a)} compared rays {p:.2f} dB"
     return int(amb.sum())
