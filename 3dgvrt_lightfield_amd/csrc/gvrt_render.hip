@@ -662,6 +662,7 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
             uint64_t bal[BVH_W];
             int32_t ch[BVH_W];
             uint32_t leafmask, dleaf = 0, lead = 0;  // leaves to test; FRONT: leaves / leading children to record
+            uint32_t capc = 0;  // FRONT: children some lane reaches only without its cap (cap-culled lanes)
             int32_t next = -1;
             [[maybe_unused]] uint64_t t_node0 = 0;
             [[maybe_unused]] bool rev = false;
@@ -706,9 +707,13 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                         bal2[k] = __builtin_amdgcn_ballot_w64(h2);
                     }
                 }
-                // children some lane hits without the cap (those no lane descends into are deferred, below)
+                // children some lane hits without the cap (those no lane descends into are deferred, below), and
+                // children with cap-culled lanes (a leaf among them is recorded even when other lanes test it)
 #pragma unroll
-                for (int k = 0; k < BVH_W; ++k) dm |= nz_bit(bal2[k], 1u << k);
+                for (int k = 0; k < BVH_W; ++k) {
+                    dm |= nz_bit(bal2[k], 1u << k);
+                    capc |= nz_bit(bal2[k] & ~bal[k], 1u << k);
+                }
             } else if (octw) {
                 // (an opaque copy of 1/d: otherwise the first child's plane FMAs, common to both tests, are hoisted
                 // above the branch and every min / max input after it gets a canonicalising v_max)
@@ -876,7 +881,9 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                     }
                 }
                 if constexpr (FRONT) {
-                    if (__builtin_amdgcn_ballot_w64(frec)) fappend(F_LEAF | (uint32_t)li);
+                    // recorded when a lane admitted a crossing (it may be pushed out of the buffer later) or a lane
+                    // was kept from testing it by its full buffer
+                    if (((capc >> k) & 1u) || __builtin_amdgcn_ballot_w64(frec)) fappend(F_LEAF | (uint32_t)li);
                 }
             }
             if constexpr (FRONT) {
