@@ -1,6 +1,7 @@
 """Traversal diagnostics of the render kernel on a bench scene (stats-enabled renders).
 
 python scripts/diag_traversal.py [config] [kbuffer depths...]
+DIAG_OPTS="frontier=1,tile_order=0" sets handle options (gvrt_set_option) first.
 """
 import importlib
 import json
@@ -18,6 +19,9 @@ waves = (W + 7) // 8 * ((H + 7) // 8)
 rays = W * H
 out = {}
 with gv.Renderer(0) as r:
+    for kv in filter(None, os.environ.get("DIAG_OPTS", "").split(",")):
+        name, _, val = kv.partition("=")
+        r.set_option(name, int(val))
     bkw = {} if os.environ.get("GVRT_BUILD") == "fast" else dict(builder=2, collapse=1)  # bench default
     r.prepare(s, split_cells=int(os.environ.get("DIAG_SPLIT", "0")), **bkw)
     runs = [("literal", gv.MODE_LITERAL, 0)] + [(f"fast_k{k}", gv.MODE_FAST, k) for k in depths]
@@ -46,5 +50,7 @@ with gv.Renderer(0) as r:
         if pc[3]:
             out[name]["phase_frac"] = {"node": round(pc[0] / pc[3], 3), "leaf+insert": round(pc[1] / pc[3], 3),
                                        "composite": round(pc[2] / pc[3], 3),
-                                       "cycles/wave": round(pc[3] / waves)}
+                                       "cycles/wave": round(pc[3] / waves),
+                                       "node_cycles/wave": round(pc[0] / waves), "leaf_cycles/wave": round(pc[1] / waves),
+                                       "composite_cycles/wave": round(pc[2] / waves)}
 print(json.dumps(out, indent=1))
