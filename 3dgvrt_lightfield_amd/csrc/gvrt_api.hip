@@ -437,6 +437,8 @@ static gvrt_status ensure_tile_order(gvrt_context* c, uint32_t tiles_x, uint32_t
     GVRT_HIP(c, hipStreamSynchronize(c->stream));  // queued launches may still read the old arrays (and
                                                     // the previous list's upload may still read h_tcode)
     gvrt_dfree(c, (void**)&c->d_tbucket);
+    gvrt_dfree(c, (void**)&c->d_tbucket2);
+    gvrt_dfree(c, (void**)&c->d_tgrid);
     gvrt_dfree(c, (void**)&c->d_thist);
     gvrt_dfree(c, (void**)&c->d_tcode);
     gvrt_dfree(c, (void**)&c->d_order);
@@ -447,7 +449,9 @@ static gvrt_status ensure_tile_order(gvrt_context* c, uint32_t tiles_x, uint32_t
     if (n == 0) return GVRT_OK;
     gvrt_status s;
     if ((s = gvrt_dalloc(c, (void**)&c->d_tbucket, n))) return s;
-    if ((s = gvrt_dalloc(c, (void**)&c->d_thist, 4 * 4 * TILE_BUCKETS))) return s;
+    if ((s = gvrt_dalloc(c, (void**)&c->d_tbucket2, n))) return s;
+    if ((s = gvrt_dalloc(c, (void**)&c->d_tgrid, (uint64_t)tiles_x * tiles_y * ncams))) return s;
+    if ((s = gvrt_dalloc(c, (void**)&c->d_thist, 4 * 5 * TILE_BUCKETS))) return s;
     if ((s = gvrt_dalloc(c, (void**)&c->d_order, 4 * n))) return s;
     if (!list) {
         // the full frame as a tile list in the render kernel's supertile order (its first launch's order)
@@ -466,11 +470,40 @@ static gvrt_status ensure_tile_order(gvrt_context* c, uint32_t tiles_x, uint32_t
     } else {
         c->ord_list = *list;
     }
-    GVRT_HIP(c, hipMemsetAsync(c->d_thist, 0, 4 * 4 * TILE_BUCKETS, c->stream));
+    GVRT_HIP(c, hipMemsetAsync(c->d_thist, 0, 4 * 5 * TILE_BUCKETS, c->stream));
+    c->ord_tx = tiles_x;
+    c->ord_ty = tiles_y;
+    c->ord_nc = ncams;
+    c->ord_prev_valid = false;
     c->ord_parity = 0;
     c->ord_n = n;
     c->ord_key = key;
     return GVRT_OK;
+}
+
+// Tiles a screen point may move between two launches (camera 0 of each): the angle between the cameras' axes
+// plus the translation seen at the eye's distance to the origin, in pixels
+// (H / (2 tan(fovy / 2)) per radian, tan(fovy / 2) = |projInverse[1][1]|), over the 8-pixel tile.  Only a
+// scheduling hint (the order never changes a pixel): 0 for a static camera.
+static int motion_radius(const float* prev, const float* cur, const float* proj_inv, uint32_t height) {
+    float ang = 0.0f;
+    for (int k = 0; k < 3; ++k) {
+        const float* a = prev + 4 * k;
+        const float* b = cur + 4 * k;
+        const float na = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+        const float nb = std::sqrt(b[0] * b[0] + b[1] * b[1] + b[2] * b[2]);
+        if (!(na > 0.0f) || !(nb > 0.0f)) return 0;
+        const float cs = std::min(1.0f, std::max(-1.0f, (a[0] * b[0] + a[1] * b[1] + a[2] * b[2]) / (na * nb)));
+        ang = std::max(ang, std::acos(cs));
+    }
+    const float dx = cur[12] - prev[12], dy = cur[13] - prev[13], dz = cur[14] - prev[14];
+    const float dist = std::sqrt(cur[12] * cur[12] + cur[13] * cur[13] + cur[14] * cur[14]);
+    const float trans = std::sqrt(dx * dx + dy * dy + dz * dz) / std::max(dist, 1e-3f);
+    const float th = std::fabs(proj_inv[5]);
+    if (!(th > 0.0f)) return 0;
+    const float px = (ang + trans) * (float)height / (2.0f * th);
+    if (!(px == px)) return 0;
+    return (int)std::min(std::ceil(px / 8.0f), 64.0f);
 }
 
 // The camera ring sized for ncams cameras per slot (regrown, after the queued frames, when a launch has more).
@@ -629,12 +662,17 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
     // cost-ordered dispatch: full frames and caller tile lists alike (the kernel renders list position
     // perm[i] in workgroup i; outputs stay where the list puts them)
     const bool ordered = c->opt[GVRT_OPT_TILE_ORDER] != 0 && nwork > 0;
+    int ord_radius = 0;  // moving camera: spread of the previous launch's tile costs (motion_radius)
     if (ordered) {
         if ((s = ensure_tile_order(c, tiles_x, tiles_y, ncams, tiles ? &c->h_tiles : nullptr))) return s;
+        if (c->ord_prev_valid) ord_radius = motion_radius(c->ord_prev_vi, view_inverse, proj_inverse, height);
+        std::memcpy(c->ord_prev_vi, view_inverse, 64);
+        c->ord_prev_valid = true;
         a.tile_bucket = c->d_tbucket;
         a.tile_hist = c->d_thist + TILE_BUCKETS * c->ord_parity;
         if (!tiles) a.tiles = c->d_tcode;
-        if (c->ord_ready) a.perm = c->d_order;
+        // a camera that moved by more than 12 tiles in one frame: the previous costs say little, supertile order
+        if (c->ord_ready && ord_radius <= 12) a.perm = c->d_order;
     }
     a.ntiles = nwork;
     const uint64_t npix = out->packed ? nwork * 64 : (uint64_t)width * height * ncams;
@@ -683,7 +721,7 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         GVRT_HIP(c, hipEventRecord(e1, c->stream));
         GVRT_HIP(c, hipEventRecord(c->cam_ev[c->cam_slot], c->stream));
         c->cam_ev_live[c->cam_slot] = true;
-        if (ordered && (s = gvrt_launch_tile_order(c))) return s;
+        if (ordered && (s = gvrt_launch_tile_order(c, a.tiles, std::min(ord_radius, 8)))) return s;
         ++c->async_pending;
         c->stats.rays = (tiles || out->packed) ? nwork * 64 : total_tiles * 64;
         return GVRT_OK;
@@ -694,7 +732,7 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
     GVRT_HIP(c, hipEventRecord(c->ev1, c->stream));
     GVRT_HIP(c, hipEventRecord(c->cam_ev[c->cam_slot], c->stream));
     c->cam_ev_live[c->cam_slot] = true;
-    if (ordered && (s = gvrt_launch_tile_order(c))) return s;
+    if (ordered && (s = gvrt_launch_tile_order(c, a.tiles, std::min(ord_radius, 8)))) return s;
     if (!out->device_ptrs) {
         if (b32) GVRT_HIP(c, hipMemcpyAsync(out->rgba32f, a.rgba32f, b32, hipMemcpyDeviceToHost, c->stream));
         if (bdir) GVRT_HIP(c, hipMemcpyAsync(out->ray_dirs, a.ray_dirs, bdir, hipMemcpyDeviceToHost, c->stream));

@@ -110,6 +110,11 @@ struct gvrt_context {
     uint32_t ord_parity = 0;         // parity of the next launch
     uint32_t* d_tcode = nullptr;     // full frames: the tile list (cam << 24 | ty << 12 | tx), supertile order
     uint32_t* d_order = nullptr;     // dispatch order: tile-list positions, costliest class first
+    uint8_t* d_tgrid = nullptr;      // moving camera: the classes on a screen grid (tiles_x x tiles_y x ncams)
+    uint8_t* d_tbucket2 = nullptr;   // moving camera: the classes spread by the motion radius
+    uint32_t ord_tx = 0, ord_ty = 0, ord_nc = 0;  // grid of the order arrays
+    float ord_prev_vi[16] = {};      // camera 0 of the previous ordered launch (motion radius)
+    bool ord_prev_valid = false;
     std::vector<uint32_t> h_tcode;   // host source of d_tcode (kept alive for its stream-ordered upload)
     void* d_stage = nullptr;  // staging for host outputs
     uint64_t stage_cap = 0;
@@ -141,7 +146,8 @@ gvrt_status gvrt_sah_build_device(gvrt_context* c, uint64_t m, const float* lbox
                                   gvrt::Bvh4Node* out4, uint32_t* depth_out, uint64_t* n4_out, uint32_t* depth4_out);
 // gvrt_render.hip
 gvrt_status gvrt_launch_render_mode(gvrt_context* c, const gvrt::RenderArgs& a, uint64_t nwaves, bool literal);
-gvrt_status gvrt_launch_tile_order(gvrt_context* c);
+// codes: the tile list the order is over (cam << 24 | ty << 12 | tx); radius > 0: classes spread by a max filter
+gvrt_status gvrt_launch_tile_order(gvrt_context* c, const uint32_t* codes, int radius);
 // record preparation: op 0 save leaf positions, 1 write kernel-frame origins for o, 2 restore positions
 gvrt_status gvrt_launch_rec_prep(gvrt_context* c, int op, const float* o);
 // the 8 octant copies of the 4-wide nodes (d_nodes4x8)

@@ -1227,14 +1227,59 @@ __global__ __launch_bounds__(256) void k_tile_order(uint32_t n, const uint8_t* _
     }
 }
 
-gvrt_status gvrt_launch_tile_order(gvrt_context* c) {
+// Moving camera: the previous frame's cost of a screen tile predicts the cost of the tiles around it in this
+// frame.  The classes are spread by a max filter of radius R tiles (R from the camera motion, render_impl) before
+// ordering, so that a costly region that moved by up to R tiles still starts early (a stale exact order put the
+// costly tiles of the moved view last: 2.04 ms vs 1.58 unordered at 2 deg per frame).
+// k_tile_scatter: the classes of the tile list into a screen grid (one byte per tile); k_tile_dilate: per list
+// position the largest class within R tiles, with the class counts for k_tile_order.
+__global__ __launch_bounds__(256) void k_tile_scatter(uint32_t n, const uint32_t* __restrict__ codes,
+                                                      const uint8_t* __restrict__ bucket, uint32_t tiles_x,
+                                                      uint32_t tiles_y, uint8_t* __restrict__ grid) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t t = codes[i];
+    grid[((uint64_t)(t >> 24) * tiles_y + ((t >> 12) & 0xFFFu)) * tiles_x + (t & 0xFFFu)] = bucket[i];
+}
+__global__ __launch_bounds__(256) void k_tile_dilate(uint32_t n, const uint32_t* __restrict__ codes,
+                                                     const uint8_t* __restrict__ grid, uint32_t tiles_x,
+                                                     uint32_t tiles_y, int radius, uint8_t* __restrict__ out,
+                                                     uint32_t* __restrict__ hist) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t t = codes[i];
+    const int tx = (int)(t & 0xFFFu), ty = (int)((t >> 12) & 0xFFFu);
+    const uint8_t* g = grid + (uint64_t)(t >> 24) * tiles_y * tiles_x;
+    const int x0 = max(0, tx - radius), x1 = min((int)tiles_x - 1, tx + radius);
+    const int y0 = max(0, ty - radius), y1 = min((int)tiles_y - 1, ty + radius);
+    uint32_t m = 0;
+    for (int y = y0; y <= y1; ++y)
+        for (int x = x0; x <= x1; ++x) m = max(m, (uint32_t)g[(uint64_t)y * tiles_x + x]);
+    out[i] = (uint8_t)m;
+    atomicAdd(hist + m, 1u);
+}
+
+gvrt_status gvrt_launch_tile_order(gvrt_context* c, const uint32_t* codes, int radius) {
     const uint32_t p = c->ord_parity;
-    uint32_t* h = c->d_thist;  // [hist 0, hist 1, fill 0, fill 1] x TILE_BUCKETS
+    uint32_t* h = c->d_thist;  // [hist 0, hist 1, fill 0, fill 1, dilated hist] x TILE_BUCKETS
     const uint32_t n = (uint32_t)c->ord_n;
     // XCD-aware dealing of each cost class (GVRT_OPT_TILE_XCD = 0: off): -2 to -4 % kernel time
     const uint32_t xcd = c->opt[GVRT_OPT_TILE_XCD] != 0;
-    hipLaunchKernelGGL(k_tile_order, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, c->d_tbucket,
-                       h + TILE_BUCKETS * p, h + TILE_BUCKETS * (2 + p), h + TILE_BUCKETS * (1 - p),
+    const uint8_t* bucket = c->d_tbucket;
+    uint32_t* hist = h + TILE_BUCKETS * p;
+    if (radius > 0 && codes) {
+        const uint64_t cells = (uint64_t)c->ord_tx * c->ord_ty * c->ord_nc;
+        GVRT_HIP(c, hipMemsetAsync(c->d_tgrid, 0, cells, c->stream));
+        GVRT_HIP(c, hipMemsetAsync(h + 4 * TILE_BUCKETS, 0, 4 * TILE_BUCKETS, c->stream));
+        hipLaunchKernelGGL(k_tile_scatter, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, codes, c->d_tbucket,
+                           c->ord_tx, c->ord_ty, c->d_tgrid);
+        hipLaunchKernelGGL(k_tile_dilate, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, codes, c->d_tgrid,
+                           c->ord_tx, c->ord_ty, radius, c->d_tbucket2, h + 4 * TILE_BUCKETS);
+        bucket = c->d_tbucket2;
+        hist = h + 4 * TILE_BUCKETS;
+    }
+    hipLaunchKernelGGL(k_tile_order, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, bucket,
+                       hist, h + TILE_BUCKETS * (2 + p), h + TILE_BUCKETS * (1 - p),
                        h + TILE_BUCKETS * (3 - p), c->d_order, xcd);
     GVRT_HIP(c, hipGetLastError());
     c->ord_parity = 1 - p;
