@@ -329,7 +329,10 @@ gvrt_status gvrt_get_device_buffers(gvrt_handle c, gvrt_device_buffers* out) {
 gvrt_status gvrt_set_option(gvrt_handle c, uint32_t option, int64_t value) {
     if (!c) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL handle");
     if (option >= GVRT_OPT_COUNT) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "unknown option");
-    if (value != 0 && value != 1) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "option values are 0 or 1");
+    const int64_t vmax = option == GVRT_OPT_ORDER_SPREAD ? 8 : 1;
+    if (value < 0 || value > vmax)
+        return gvrt_fail(c, GVRT_ERR_INVALID_ARG, option == GVRT_OPT_ORDER_SPREAD ? "order spread is 0..8 tiles"
+                                                                                  : "option values are 0 or 1");
     if (c->opt[option] == value) return GVRT_OK;
     GVRT_HIP(c, hipSetDevice(c->device));
     if (c->async_pending) GVRT_HIP(c, hipStreamSynchronize(c->stream));  // queued launches used the old value
@@ -666,6 +669,7 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
     if (ordered) {
         if ((s = ensure_tile_order(c, tiles_x, tiles_y, ncams, tiles ? &c->h_tiles : nullptr))) return s;
         if (c->ord_prev_valid) ord_radius = motion_radius(c->ord_prev_vi, view_inverse, proj_inverse, height);
+        ord_radius = std::max(ord_radius, (int)c->opt[GVRT_OPT_ORDER_SPREAD]);
         std::memcpy(c->ord_prev_vi, view_inverse, 64);
         c->ord_prev_valid = true;
         a.tile_bucket = c->d_tbucket;

@@ -247,7 +247,7 @@ typedef struct {
 gvrt_status gvrt_get_device_buffers(gvrt_handle h, gvrt_device_buffers* out);
 
 /* Per-handle tuning switches: the measured-best defaults; each exists so that a same-box
- * A/B can turn one choice off.  None of them changes an image. */
+ * A/B can turn one choice off.  None of them changes an image.  Values are 0 or 1 except where stated. */
 #define GVRT_OPT_TILE_ORDER 0u      /* 1 (default): tiles dispatched costliest first by the previous launch's
                                        per-tile costs; 0: supertile order */
 #define GVRT_OPT_TILE_XCD 1u        /* 1 (default): each cost class dealt to the 8 XCDs in contiguous chunks */
@@ -261,7 +261,10 @@ gvrt_status gvrt_get_device_buffers(gvrt_handle h, gvrt_device_buffers* out);
 #define GVRT_OPT_FRONTIER 6u        /* 1 (default): FAST round r + 1 traverses round r's frontier (the nodes culled
                                        only by a full k-buffer and the leaves that gave a crossing) instead of
                                        restarting from the root; same crossings in the same order */
-#define GVRT_OPT_COUNT 7u
+#define GVRT_OPT_ORDER_SPREAD 7u    /* 0..8 (default 0): the least radius, in tiles, by which the previous launch's
+                                       tile costs are spread (max filter) before ordering; the camera's motion sets
+                                       it otherwise (0 for a static camera) */
+#define GVRT_OPT_COUNT 8u
 gvrt_status gvrt_set_option(gvrt_handle h, uint32_t option, int64_t value);
 gvrt_status gvrt_get_option(gvrt_handle h, uint32_t option, int64_t* value);
 

@@ -540,7 +540,7 @@ def test_unpacked_fast_path_matches(gv, config1):
 
 
 @pytest.mark.parametrize("option", ["tile_order", "tile_xcd", "octant_nodes", "record_origins", "box_slack",
-                                    "frontier"])
+                                    "frontier", "order_spread"])
 def test_tuning_options_change_no_pixel(gv, config1, option):
     """Each per-handle tuning switch (gvrt_set_option) changes how the frame is computed, never a pixel:
     the frame with the switch flipped equals the default frame bit for bit (two launches each, so the
@@ -555,7 +555,7 @@ def test_tuning_options_change_no_pixel(gv, config1, option):
         assert r.get_option(option) == 1 - default
         got = [r.render(vi, pi, W, H)["rgba32f"] for _ in range(2)]
         with pytest.raises(gv.GvrtError):
-            r.set_option(option, 2)
+            r.set_option(option, 9 if option == "order_spread" else 2)
     for a, b in zip(ref, got):
         np.testing.assert_array_equal(a, b)
 
