@@ -121,7 +121,7 @@ struct gvrt_context {
 
     gvrt_stats stats{};
     // per-handle tuning switches (gvrt_set_option), measured-best defaults
-    int64_t opt[GVRT_OPT_COUNT] = {1, 1, 1, 1, 0, 1, 0, 0};
+    int64_t opt[GVRT_OPT_COUNT] = {1, 1, 1, 1, 0, 1, 0};
 };
 
 gvrt_status gvrt_fail(gvrt_context* c, gvrt_status code, const std::string& msg);

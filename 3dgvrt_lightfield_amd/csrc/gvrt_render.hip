@@ -83,43 +83,6 @@ __device__ inline bool box_hit_nf(float nx, float ny, float nz, float fx, float 
     else return tn <= tf;
 }
 
-// box_hit_nf against two far limits at once: h1 under t1 (the k-buffer cap included), h2 under t2 (without it).
-// h1 is bit for bit box_hit_nf's result (float min is exact, so the grouping of the far-plane minimum is free).
-template <bool SLACK>
-__device__ inline void box_hit_nf2(float nx, float ny, float nz, float fx, float fy, float fz, f3 oinv, f3 inv, float t0,
-                                   float t1, float t2, bool& h1, bool& h2) {
-    const float an = fmaf(nx, inv.x, -oinv.x), af = fmaf(fx, inv.x, -oinv.x);
-    const float bn = fmaf(ny, inv.y, -oinv.y), bf = fmaf(fy, inv.y, -oinv.y);
-    const float cn = fmaf(nz, inv.z, -oinv.z), cf = fmaf(fz, inv.z, -oinv.z);
-    const float tn = fmaxf(fmaxf(t0, an), fmaxf(bn, cn));
-    const float tfp = fminf(af, fminf(bf, cf));
-    const float tf1 = fminf(t1, tfp), tf2 = fminf(t2, tfp);
-    if constexpr (SLACK) {
-        h1 = tn <= tf1 + 2e-6f * fabsf(tf1);
-        h2 = tn <= tf2 + 2e-6f * fabsf(tf2);
-    } else {
-        h1 = tn <= tf1;
-        h2 = tn <= tf2;
-    }
-}
-template <bool SLACK>
-__device__ inline void box_hit2(float lx, float ly, float lz, float hx, float hy, float hz, f3 oinv, f3 inv, float t0,
-                                float t1, float t2, bool& h1, bool& h2) {
-    const float ax = fmaf(lx, inv.x, -oinv.x), bx = fmaf(hx, inv.x, -oinv.x);
-    const float ay = fmaf(ly, inv.y, -oinv.y), by = fmaf(hy, inv.y, -oinv.y);
-    const float az = fmaf(lz, inv.z, -oinv.z), bz = fmaf(hz, inv.z, -oinv.z);
-    const float tn = fmaxf(fmaxf(t0, fminf(ax, bx)), fmaxf(fminf(ay, by), fminf(az, bz)));
-    const float tfp = fminf(fmaxf(ax, bx), fminf(fmaxf(ay, by), fmaxf(az, bz)));
-    const float tf1 = fminf(t1, tfp), tf2 = fminf(t2, tfp);
-    if constexpr (SLACK) {
-        h1 = tn <= tf1 + 2e-6f * fabsf(tf1);
-        h2 = tn <= tf2 + 2e-6f * fabsf(tf2);
-    } else {
-        h1 = tn <= tf1;
-        h2 = tn <= tf2;
-    }
-}
-
 // Insert two crossings of one proxy (a.t <= b.t, either may be INF_DIST) in one pass.  Per slot the
 // same strict-< rule as compareAndSwapHitPayloadValue (ties keep the earlier arrival first).
 template <int K>
@@ -421,22 +384,7 @@ __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlan
 constexpr uint32_t ST_W = 8, ST_H = 4;
 constexpr int RENDER_MIN_WAVES = 4;
 
-// Frontier traversal (FRONT kernels, FAST packed k-buffer).  Round r + 1 of a wave does not restart
-// from the root: it traverses round r's frontier, the list of (a) children no lane descended into only because of
-// a lane's full k-buffer (hit within (tlo, min(thi, tcut)] but beyond kt[K-1]), and (b) leaves that gave some
-// lane an admitted crossing (it may have been pushed out of the buffer later).  Every crossing round r + 1 needs
-// lies under such an entry: it is beyond its lane's last composited slot, so it was either culled by that lane's
-// buffer cap (a) or found and then left out of the buffer (b); leaves of (b) whose crossings were composited are
-// re-tested once and give nothing (t <= last).  Entries are recorded in the DFS order a root restart would meet
-// them (deferred children ride on the stack and are recorded when popped; a node's leaves before its children),
-// so the k-buffer sees the same insertions in the same order: the image, ties included, is the root restart's.
-// The lists live in LDS (two of FCAP entries, by round parity); a round whose list overflows is followed by a
-// root restart.
-constexpr uint32_t FCAP = 384;
-constexpr uint32_t F_LEAF = 0x40000000u;   // entry: a leaf slot (else a node index)
-constexpr uint32_t F_DEFER = 0x20000000u;  // stack entry: a deferred child, recorded when popped
-
-template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK, bool SLACK, bool OKREC, bool FRONT>
+template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK, bool SLACK, bool OKREC>
 __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArgs a, const Bvh4Node* __restrict__ nodes_,
                                                                  const RenderRec* __restrict__ recs_,
                                                                  const RenderRec* __restrict__ crecs_,
@@ -461,8 +409,6 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
     __shared__ uint32_t s_pxy[64];  // px | py << 16, parked for the output stage (not live in VGPRs)
     __shared__ unsigned long long s_t0;  // wave start (s_memtime), for the per-tile cost class
     __shared__ int32_t s_stack[STACK_DEPTH];
-    __shared__ uint32_t s_front[FRONT ? 2 : 1][FRONT ? FCAP : 1];  // frontier lists by round parity
-    static_assert(!FRONT || (PACK && !LITERAL), "frontier traversal: FAST packed kernels");
     // lane from mbcnt (no register input)
     const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 #define LL (PACK ? launder_lane(lane) : lane)  // FAST kernels only: LITERAL spilled more with it
@@ -568,30 +514,6 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
     int sp = 0;
     auto push = [&](int32_t v) { stack[sp++] = v; };
     auto pop = [&]() -> int32_t { return unii(stack[--sp]); };
-    // frontier state (FRONT): entries of the list being read (fr_n, cursor fr_rd) and of the one being written
-    // (fw_n, fw_ok: it did not overflow), by round parity fpar (written list fpar, read list fpar ^ 1)
-    uint32_t fr_n = 0, fr_rd = 0, fw_n = 0, fpar = 0;
-    bool fw_ok = false;
-    auto fappend = [&](uint32_t e) {
-        if (fw_n < FCAP) s_front[FRONT ? fpar : 0][FRONT ? fw_n : 0] = e;
-        else fw_ok = false;
-        ++fw_n;
-    };
-    // the next entry to visit: the stack, then the frontier being read; deferred stack entries are recorded for
-    // the next round on the way (-1: the round's traversal is done)
-    auto next_entry = [&]() -> int32_t {
-        while (true) {
-            int32_t e;
-            if (sp > 0) e = pop();
-            else if (FRONT && fr_rd < fr_n) e = unii((int32_t)s_front[FRONT ? (fpar ^ 1u) : 0][FRONT ? fr_rd++ : 0]);
-            else return -1;
-            if (FRONT && ((uint32_t)e & F_DEFER)) {
-                fappend((uint32_t)e & ~F_DEFER);
-                continue;
-            }
-            return e;
-        }
-    };
     {
         // radianceFromSpH basis factors (gaussianfunctions.glsl:122-151), signs folded, zero past
         // sph_eval_degree; computed once per ray and kept in LDS (not registers) through the traversal
@@ -646,34 +568,9 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
         sp = 0;
         int32_t cur = 0;  // node index (wave-uniform); the node is fetched at the top of each visit so its
                           // 32 SGPRs are not loop-carried
-        if constexpr (FRONT) {
-            // the previous round's frontier replaces the root unless it overflowed (or this is the first round)
-            const bool use = fw_ok;
-            fr_n = use ? fw_n : 0;
-            fr_rd = 0;
-            fpar ^= 1u;
-            fw_n = 0;
-            fw_ok = true;
-            if (use) cur = next_entry();
-        }
         if constexpr (STATS) ++w_rounds;
-        if (!FRONT || cur >= 0)
         while (true) {
-            uint64_t bal[BVH_W];
-            int32_t ch[BVH_W];
-            uint32_t leafmask, dleaf = 0, lead = 0;  // leaves to test; FRONT: leaves / leading children to record
-            uint32_t capc = 0;  // FRONT: children some lane reaches only without its cap (cap-culled lanes)
-            int32_t next = -1;
             [[maybe_unused]] uint64_t t_node0 = 0;
-            [[maybe_unused]] bool rev = false;
-            if (FRONT && ((uint32_t)cur & F_LEAF)) {
-                // a leaf entry of the frontier: tested by every lane (a lane that misses its box has no crossing)
-                leafmask = 1u;
-                ch[0] = ~(int32_t)((uint32_t)cur & ~F_LEAF);
-                bal[0] = ~0ull;
-                next = next_entry();
-                if constexpr (STATS) t_node0 = __builtin_amdgcn_s_memtime();
-            } else {
             if constexpr (STATS) {
                 ++w_nodes;
                 w_late += w_rounds > 1 ? 1u : 0u;
@@ -681,40 +578,8 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
             }
             const NodeS nd = load_node_at(nbase, unii(cur));  // whole node: 2x s_load_dwordx16
             const float tc = fminf(fminf(thi, kt[KB - 1]), tcut);
-            // FRONT: a child is deferred when some lane would descend into it but for its full buffer
-            [[maybe_unused]] const float tc2 = fminf(thi, tcut);
-            uint32_t dm = 0;
-            if (FRONT && __builtin_amdgcn_ballot_w64(kt[KB - 1] < tc2)) {
-                uint64_t bal2[BVH_W];
-                if (octw) {
-                    f3 iv = inv;
-                    asm("" : "+v"(iv.x), "+v"(iv.y), "+v"(iv.z));
-#pragma unroll
-                    for (int k = 0; k < BVH_W; ++k) {
-                        bool h1, h2;
-                        box_hit_nf2<SLACK>(NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 1),
-                                           NODE_BOX(nd, k, 3), NODE_BOX(nd, k, 5), oinv, iv, tlo, tc, tc2, h1, h2);
-                        bal[k] = __builtin_amdgcn_ballot_w64(h1);
-                        bal2[k] = __builtin_amdgcn_ballot_w64(h2);
-                    }
-                } else {
-#pragma unroll
-                    for (int k = 0; k < BVH_W; ++k) {
-                        bool h1, h2;
-                        box_hit2<SLACK>(NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 1),
-                                        NODE_BOX(nd, k, 3), NODE_BOX(nd, k, 5), oinv, inv, tlo, tc, tc2, h1, h2);
-                        bal[k] = __builtin_amdgcn_ballot_w64(h1);
-                        bal2[k] = __builtin_amdgcn_ballot_w64(h2);
-                    }
-                }
-                // children some lane hits without the cap (those no lane descends into are deferred, below), and
-                // children with cap-culled lanes (a leaf among them is recorded even when other lanes test it)
-#pragma unroll
-                for (int k = 0; k < BVH_W; ++k) {
-                    dm |= nz_bit(bal2[k], 1u << k);
-                    capc |= nz_bit(bal2[k] & ~bal[k], 1u << k);
-                }
-            } else if (octw) {
+            uint64_t bal[BVH_W];
+            if (octw) {
                 // (an opaque copy of 1/d: otherwise the first child's plane FMAs, common to both tests, are hoisted
                 // above the branch and every min / max input after it gets a canonicalising v_max)
                 f3 iv = inv;
@@ -731,6 +596,7 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                         box_hit<SLACK>(NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 1),
                                        NODE_BOX(nd, k, 3), NODE_BOX(nd, k, 5), oinv, inv, tlo, tc));
             }
+            int32_t ch[BVH_W];
 #pragma unroll
             for (int k = 0; k < BVH_W; ++k) ch[k] = unii(NODE_CHILD(nd, k));
             // ---- children in the node's stored order (in-order of the binary split), forward when the
@@ -742,65 +608,34 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
             for (int k = 0; k < BVH_W; ++k) hm |= nz_bit(bal[k], 1u << k);
             if constexpr (STATS) w_dead += hm == 0 ? 1u : 0u;
             const uint32_t inner = uni(NODE_PAD(nd, 1));
-            leafmask = hm & ~inner;
+            uint32_t leafmask = hm & ~inner;
             uint32_t im = hm & inner;
-            if constexpr (FRONT) {
-                dm &= ~hm;  // deferred: hit by some lane without its cap, descended into by none
-                dleaf = dm & ~inner;
-                const uint32_t dmi = dm & inner;
-                uint32_t cm = im | dmi;
-                if (cm) {
-                    rev = (rsign >> uni(NODE_PAD(nd, 0))) & 1u;
-                    // deferred children before the first descended one (in visiting order) are recorded after
-                    // this node's leaves; the ones after it ride on the stack with the rest
-                    while (cm) {
-                        const int first = rev ? 31 - __clz(cm) : __ffs(cm) - 1;
-                        cm &= ~(1u << first);
-                        if ((im >> first) & 1u) {
-                            next = GVRT_PICK(ch, first);
-                            break;
-                        }
-                        lead |= 1u << first;
-                    }
-                    while (cm) {  // the next child in visiting order ends on top
-                        const int k = rev ? __ffs(cm) - 1 : 31 - __clz(cm);
-                        push(GVRT_PICK(ch, k) | (((dmi >> k) & 1u) ? (int32_t)F_DEFER : 0));
-                        cm &= ~(1u << k);
-                    }
-                }
-                // (next stays -1 when nothing is descended: the next entry is taken after the leaves)
-            } else if (im) {
-                const bool rv = (rsign >> uni(NODE_PAD(nd, 0))) & 1u;
-                const int first = rv ? 31 - __clz(im) : __ffs(im) - 1;
+            int32_t next = -1;
+            if (im) {
+                const bool rev = (rsign >> uni(NODE_PAD(nd, 0))) & 1u;
+                const int first = rev ? 31 - __clz(im) : __ffs(im) - 1;
                 next = GVRT_PICK(ch, first);
                 im &= ~(1u << first);
                 while (im) {  // the next child in visiting order ends on top
-                    const int k = rv ? __ffs(im) - 1 : 31 - __clz(im);
+                    const int k = rev ? __ffs(im) - 1 : 31 - __clz(im);
                     push(GVRT_PICK(ch, k));
                     im &= ~(1u << k);
                 }
             } else if (sp > 0) {
                 next = pop();
             }
-            }  // node entry
             [[maybe_unused]] uint64_t t_leaf0 = 0;
             if constexpr (STATS) {
                 t_leaf0 = __builtin_amdgcn_s_memtime();
                 cyc_node += t_leaf0 - t_node0;
             }
             // ---- leaves of this node (the k-buffer orders them); one rolled loop = one insertion site
-            if constexpr (FRONT) leafmask |= dleaf;
 #pragma unroll 1
             while (leafmask) {
                 const int k = __builtin_ctz(leafmask);
                 leafmask &= leafmask - 1;
-                const int32_t li = ~GVRT_PICK(ch, k);  // leaf slot
-                if (FRONT && ((dleaf >> k) & 1u)) {  // deferred leaf child: recorded, not tested
-                    fappend(F_LEAF | (uint32_t)li);
-                    continue;
-                }
                 const uint64_t bk = GVRT_PICK(bal, k);
-                [[maybe_unused]] bool frec = false;  // FRONT: this lane admitted a crossing of the leaf
+                const int32_t li = ~GVRT_PICK(ch, k);  // leaf slot
                 const RenderRec rec = load_rec_at(recs_, unii(li));
                 // split (SplitBLAS analogue): the piece's proxy id and cell; cell == ~0u admits every crossing
                 uint4 pa = make_uint4((uint32_t)li, 0xFFFFFFFFu, 0u, 0u);
@@ -818,21 +653,7 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                         // 1e-3 margin), so most proxies are rejected without the sqrt / exp below.
                         const float l2 = len2(dk);
                         const f3 cu = cross3(dk, ok);
-                        bool maybe = (cu.x * cu.x + cu.y * cu.y + cu.z * cu.z) < a.gpre * l2;
-                        if constexpr (!LITERAL && !ADAPTIVE) {
-                            // Conservative t-range pre-test: the proxy lies inside the kernel-frame sphere of radius
-                            // 1.2584 kS < hk = sqrt(3) kS, so both crossings lie within hk / |dk| of the closest
-                            // approach tq = -(ok . dk) / |dk|^2 (37 % margin, plus 1e-5 relative).  A lane whose
-                            // crossings all lie at or before tlo (composited in an earlier round: a revisited leaf)
-                            // or beyond its cull distance (full buffer, termination) skips the response and clip
-                            // that could not admit anything.  (FRONT: only the tlo side; a lane kept out by its
-                            // cap must still reach the leaf's recording.)
-                            const float ri = __builtin_amdgcn_rsqf(l2);
-                            const float tq = -(ok.x * dk.x + ok.y * dk.y + ok.z * dk.z) * (ri * ri);
-                            const float hh = a.kernel_h * ri + 1e-5f * fabsf(tq);
-                            maybe = maybe && tq + hh > tlo;
-                            if constexpr (!FRONT) maybe = maybe && tq - hh < fminf(fminf(thi, kt[KB - 1]), tcut);
-                        }
+                        const bool maybe = (cu.x * cu.x + cu.y * cu.y + cu.z * cu.z) < a.gpre * l2;
                         bool acc = false;
                         float galpha = 0.0f;
                         if (maybe) acc = particle_alpha(ok, dk, l2, rec.density, a.min_response, a.alpha_min, galpha);
@@ -853,7 +674,6 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                                 }
                                 const float ta = in0 && tn < tcut ? tn : (in1 && tf < tcut ? tf : INF_DIST);
                                 const float tb = (in0 && in1 && tf < tcut) ? tf : INF_DIST;
-                                if constexpr (FRONT) frec = ta < INF_DIST;
                                 if (ta < kt[KB - 1]) {
                                   if constexpr (PACK) {
                                     const uint32_t q = alpha_code(galpha);
@@ -894,20 +714,6 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                         }
                     }
                 }
-                if constexpr (FRONT) {
-                    // recorded when a lane admitted a crossing (it may be pushed out of the buffer later) or a lane
-                    // was kept from testing it by its full buffer
-                    if (((capc >> k) & 1u) || __builtin_amdgcn_ballot_w64(frec)) fappend(F_LEAF | (uint32_t)li);
-                }
-            }
-            if constexpr (FRONT) {
-                // leading deferred children (visiting order), then the next entry when this node descends nowhere
-                while (lead) {
-                    const int k = rev ? 31 - __clz(lead) : __ffs(lead) - 1;
-                    lead &= ~(1u << k);
-                    fappend((uint32_t)GVRT_PICK(ch, k));
-                }
-                if (next < 0) next = next_entry();
             }
             if constexpr (STATS) cyc_leaf += __builtin_amdgcn_s_memtime() - t_leaf0;
             if (next < 0) break;
@@ -1113,12 +919,11 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
     // every pointer is its own __restrict__ argument: the uniform node / record loads can then be
     // proven unclobbered by the output stores and are emitted as scalar (s_load) loads
 #define KARGS a.nodes, a.recs, a.crecs, a.aux, a.sh, a.view_inv, a.tiles, a.rgba8, a.rgba32f, a.ray_dirs, a.hit_counts, a.stats
-#define GVRT_LAUNCH_SOF(L, A, K, P, S, O, F)                                                                \
-    do {                                                                                                     \
-        if (a.stats) hipLaunchKernelGGL((k_render<L, A, K, true, P, S, O, F>), g, b, 0, c->stream, a, KARGS);   \
-        else hipLaunchKernelGGL((k_render<L, A, K, false, P, S, O, F>), g, b, 0, c->stream, a, KARGS);          \
+#define GVRT_LAUNCH_SO(L, A, K, P, S, O)                                                                  \
+    do {                                                                                                  \
+        if (a.stats) hipLaunchKernelGGL((k_render<L, A, K, true, P, S, O>), g, b, 0, c->stream, a, KARGS);   \
+        else hipLaunchKernelGGL((k_render<L, A, K, false, P, S, O>), g, b, 0, c->stream, a, KARGS);          \
     } while (0)
-#define GVRT_LAUNCH_SO(L, A, K, P, S, O) GVRT_LAUNCH_SOF(L, A, K, P, S, O, false)
 #define GVRT_LAUNCH(L, A, K, P) GVRT_LAUNCH_SO(L, A, K, P, true, false)
     // FAST packed kernels also come without the per-child box slack, used when the absolute box padding
     // covers the plane rounding for this launch's cameras (RenderArgs::box_exact, set by render_impl)
@@ -1130,9 +935,6 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
     // packed payload needs record ids below 2^24 - 1 (id << 8 | q, all-ones = empty slot); the handle
     // option GVRT_OPT_PACKED_KBUFFER = 0 forces the unpacked path, which larger scenes take, for testing
     const bool pack = a.nrecs < 0xFFFFFFu && c->opt[GVRT_OPT_PACKED_KBUFFER] != 0;
-    // frontier traversal: the default FAST depth on unsplit scenes (a piece of a split proxy is no leaf slot of
-    // its own record)
-    const bool front = c->opt[GVRT_OPT_FRONTIER] != 0 && !a.aux;
     if (literal) {  // the reference's 16-slot k-buffer (MAX_HIT_PER_TRACE)
         if (adaptive) GVRT_LAUNCH(true, true, K_HITS, false);
         else GVRT_LAUNCH(true, false, K_HITS, false);
@@ -1152,26 +954,15 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
             default:
                 // the default depth also reads kernel-frame origins from the records when render_impl
                 // prepared them for a single-origin launch (RenderArgs::okrec)
-                // and traverses round r + 1 from round r's frontier (GVRT_OPT_FRONTIER)
-                if (front) {
-                    if (a.okrec && a.box_exact) GVRT_LAUNCH_SOF(false, false, K_FAST_DEFAULT, true, false, true, true);
-                    else if (a.okrec) GVRT_LAUNCH_SOF(false, false, K_FAST_DEFAULT, true, true, true, true);
-                    else if (a.box_exact) GVRT_LAUNCH_SOF(false, false, K_FAST_DEFAULT, true, false, false, true);
-                    else GVRT_LAUNCH_SOF(false, false, K_FAST_DEFAULT, true, true, false, true);
-                } else if (a.okrec && a.box_exact) {
-                    GVRT_LAUNCH_SO(false, false, K_FAST_DEFAULT, true, false, true);
-                } else if (a.okrec) {
-                    GVRT_LAUNCH_SO(false, false, K_FAST_DEFAULT, true, true, true);
-                } else {
-                    GVRT_LAUNCH_F(K_FAST_DEFAULT);
-                }
+                if (a.okrec && a.box_exact) GVRT_LAUNCH_SO(false, false, K_FAST_DEFAULT, true, false, true);
+                else if (a.okrec) GVRT_LAUNCH_SO(false, false, K_FAST_DEFAULT, true, true, true);
+                else GVRT_LAUNCH_F(K_FAST_DEFAULT);
                 break;
         }
     }
 #undef GVRT_LAUNCH
 #undef GVRT_LAUNCH_F
 #undef GVRT_LAUNCH_SO
-#undef GVRT_LAUNCH_SOF
 #undef KARGS
     GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;

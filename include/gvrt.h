@@ -258,13 +258,10 @@ gvrt_status gvrt_get_device_buffers(gvrt_handle h, gvrt_device_buffers* out);
                                        cover the plane rounding for the launch's cameras; 1: always */
 #define GVRT_OPT_PACKED_KBUFFER 5u  /* 1 (default): packed FAST k-buffer when record ids fit 24 bits; 0: the
                                        unpacked FAST kernel that larger scenes take */
-#define GVRT_OPT_FRONTIER 6u        /* 1 (default): FAST round r + 1 traverses round r's frontier (the nodes culled
-                                       only by a full k-buffer and the leaves that gave a crossing) instead of
-                                       restarting from the root; same crossings in the same order */
-#define GVRT_OPT_ORDER_SPREAD 7u    /* 0..8 (default 0): the least radius, in tiles, by which the previous launch's
+#define GVRT_OPT_ORDER_SPREAD 6u    /* 0..8 (default 0): the least radius, in tiles, by which the previous launch's
                                        tile costs are spread (max filter) before ordering; the camera's motion sets
                                        it otherwise (0 for a static camera) */
-#define GVRT_OPT_COUNT 8u
+#define GVRT_OPT_COUNT 7u
 gvrt_status gvrt_set_option(gvrt_handle h, uint32_t option, int64_t value);
 gvrt_status gvrt_get_option(gvrt_handle h, uint32_t option, int64_t* value);
 

@@ -540,7 +540,7 @@ def test_unpacked_fast_path_matches(gv, config1):
 
 
 @pytest.mark.parametrize("option", ["tile_order", "tile_xcd", "octant_nodes", "record_origins", "box_slack",
-                                    "frontier", "order_spread"])
+                                    "order_spread"])
 def test_tuning_options_change_no_pixel(gv, config1, option):
     """Each per-handle tuning switch (gvrt_set_option) changes how the frame is computed, never a pixel:
     the frame with the switch flipped equals the default frame bit for bit (two launches each, so the
@@ -558,32 +558,3 @@ def test_tuning_options_change_no_pixel(gv, config1, option):
             r.set_option(option, 9 if option == "order_spread" else 2)
     for a, b in zip(ref, got):
         np.testing.assert_array_equal(a, b)
-
-
-@pytest.mark.parametrize("cfg", ["dense", "bicycle"])
-def test_frontier_traversal_same_frames_fewer_visits(gv, cfg):
-    """Frontier traversal (GVRT_OPT_FRONTIER): round r + 1 walks round r's frontier instead of the root.  It meets
-    the same crossings in the same order, so the full 1080p frame is bit-identical to the root restart's (ties
-    included), with the same rounds per ray and fewer node visits (the dense stand-in: ~4 rounds per wave)."""
-    gen, W, H, _ = gv.scene.CONFIGS[cfg]
-    s = gv.scene.make(**gen)
-    vi, pi = gv.scene.mipnerf_camera(W, H)
-    out = {}
-    with gv.Renderer(0) as r:
-        r.prepare(s, builder=2, collapse=1)
-        for f in (0, 1):
-            r.set_option("frontier", f)
-            img = r.render(vi, pi, W, H, hit_counts=True)
-            r.set_stats(True)
-            r.render(vi, pi, W, H, rgba8=False, rgba32f=False)
-            out[f] = (img, r.stats())
-            r.set_stats(False)
-    (a, sa), (b, sb) = out[0], out[1]
-    np.testing.assert_array_equal(a["rgba32f"], b["rgba32f"])
-    np.testing.assert_array_equal(a["hit_counts"], b["hit_counts"])
-    assert sa["rounds"] == sb["rounds"] and sa["wave_rounds"] == sb["wave_rounds"]
-    record_parity(f"frontier_{cfg}", nodes_root=sa["wave_node_visits"], nodes_frontier=sb["wave_node_visits"],
-                  leaves_root=sa["wave_leaf_visits"], leaves_frontier=sb["wave_leaf_visits"],
-                  waves=((W + 7) // 8) * ((H + 7) // 8), wave_rounds=sa["wave_rounds"])
-    if cfg == "dense":
-        assert sb["wave_node_visits"] < 0.8 * sa["wave_node_visits"], (sa["wave_node_visits"], sb["wave_node_visits"])
