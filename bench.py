@@ -509,6 +509,22 @@ def main():
                              "frac_beyond_1e-4_off_threshold": float((d[~amb] > 1e-4).mean()) if (~amb).any() else 0.0,
                              "frac_beyond_1e-4_all": float((d > 1e-4).mean())}
 
+        # moving camera: the same views rendered as static frames (each view twice in a row, the second launch
+        # ordered by its own costs), so the moving-camera penalty is measured on equal work
+        orbit_static = None
+        if args.camera_path == "orbit" and world == 1:
+            import torch
+            buf = torch.zeros((part_sizes[0],) + item_shape, dtype=torch.uint8, device=dev)
+            ks = list(range(1 + args.warmup, nframes, max(1, args.steps // 10)))
+            got = []
+            for k in ks:
+                for _ in range(2):
+                    r.render_device(frame_vi[k], pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=buf.data_ptr(),
+                                    packed=packed)
+                got.append(r.render_ms())
+            orbit_static = {"kernel_ms": round(float(np.mean(got)), 4), "views": len(ks),
+                            "note": "every ~10th timed view rendered twice as a static frame (second launch ordered by "
+                                    "its own costs): the static cost of the same views"}
         balance = None
         if args.rank_balance > 1 and world == 1:
             if args.split == "views" and views > args.rank_balance:
@@ -562,6 +578,8 @@ def main():
         }
         if balance:
             result["rank_balance"] = balance
+        if orbit_static:
+            result["orbit_same_views_static"] = orbit_static
         if lit_stats:
             result["reference_counters"] = {"crossings_per_ray": lit_stats["crossings"] / (W * H),
                                             "accepted_per_ray": lit_stats["accepted"] / (W * H),
