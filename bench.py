@@ -146,11 +146,14 @@ def pmc_passes(args):
             if r.returncode != 0 or not files:
                 out.setdefault("error", f"pass {counters}: rc {r.returncode} {r.stderr[-300:]}")
                 break
+            # the timed launches only: FAST k_render dispatches of the frame's grid (config 5's per-view
+            # calibration renders and any LITERAL counter launch have other grids / kernels)
+            rows = [row for f in files for row in csv.DictReader(open(f))
+                    if "k_render<false" in row.get("Kernel_Name", "")]
+            grid = max((int(row.get("Grid_Size", 0) or 0) for row in rows), default=0)
             agg, cnt = {}, {}
-            for f in files:
-                for row in csv.DictReader(open(f)):
-                    if "k_render" not in row.get("Kernel_Name", ""):
-                        continue
+            for row in rows:
+                if int(row.get("Grid_Size", 0) or 0) == grid:
                     k = row["Counter_Name"]
                     agg[k] = agg.get(k, 0.0) + float(row["Counter_Value"])
                     cnt[k] = cnt.get(k, 0) + 1
