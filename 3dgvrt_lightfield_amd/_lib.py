@@ -139,6 +139,7 @@ SIGNATURES = {
     "gvrt_get_stats": (C.c_int32, [H, _P(Stats)]),
     "gvrt_unpack_tiles_rgba8": (C.c_int32, [H, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
                                             C.c_uint32, C.c_void_p]),
+    "gvrt_read_tile_costs": (C.c_int32, [H, C.c_void_p, C.c_uint64]),
     "gvrt_ply_load": (C.c_int32, [C.c_char_p, _P(SplatBuffers)]),
     "gvrt_ply_free": (None, [_P(SplatBuffers)]),
     "gvrt_ply_save": (C.c_int32, [C.c_char_p, _P(Splats)]),

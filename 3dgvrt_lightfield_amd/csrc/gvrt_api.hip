@@ -348,6 +348,34 @@ gvrt_status gvrt_get_option(gvrt_handle c, uint32_t option, int64_t* value) {
     return GVRT_OK;
 }
 
+static gvrt_status finish_async(gvrt_context* c);
+
+gvrt_status gvrt_read_tile_costs(gvrt_handle c, uint8_t* out, uint64_t n) {
+    if (!c || !out) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL argument");
+    if (!c->d_tbucket || c->ord_key == 0 || !c->ord_ready)
+        return gvrt_fail(c, GVRT_ERR_STATE, "no cost-ordered launch has run");
+    if (n != c->ord_n) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "n is not the tile count of the last ordered launch");
+    GVRT_HIP(c, hipSetDevice(c->device));
+    if (c->async_pending || c->async_drained) {
+        gvrt_status s = finish_async(c);
+        if (s) return s;
+    }
+    std::vector<uint8_t> cls(n);
+    GVRT_HIP(c, hipMemcpyAsync(cls.data(), c->d_tbucket, n, hipMemcpyDeviceToHost, c->stream));
+    GVRT_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->ord_list.empty() && c->h_tcode.size() == n) {
+        // full frame: list position i holds tile h_tcode[i] (cam << 24 | ty << 12 | tx)
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint32_t t = c->h_tcode[i];
+            const uint64_t cam = t >> 24, ty = (t >> 12) & 0xFFFu, tx = t & 0xFFFu;
+            out[(cam * c->ord_ty + ty) * c->ord_tx + tx] = cls[i];
+        }
+    } else {
+        std::memcpy(out, cls.data(), n);
+    }
+    return GVRT_OK;
+}
+
 gvrt_status gvrt_set_stats(gvrt_handle c, int enable) {
     if (!c) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL handle");
     c->stats_on = enable != 0;

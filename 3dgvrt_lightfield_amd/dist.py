@@ -28,6 +28,33 @@ def rank_tiles(width, height, ncams, world, block=8):
     return [tiles_for_rank(width, height, ncams, r, world, block) for r in range(world)]
 
 
+def cost_weights(classes):
+    """Relative cost of a tile from its class (gvrt_read_tile_costs: 4 classes per octave of wave cycles)."""
+    return np.exp2(np.asarray(classes, np.float64) / 4.0)
+
+
+def band_tiles(width, height, world, costs=None, ncams=1):
+    """Contiguous parts of the row-major tile order of each camera, one per rank: equal tile counts, or equal
+    summed cost when `costs` (per-tile weights [ncams, ty, tx], e.g. cost_weights of a previous frame's classes)
+    is given.  A part is a compact screen band (its tiles share BVH nodes and records in that GPU's caches),
+    where the 64x64-block round-robin of rank_tiles scatters each part over the whole frame.  Every rank
+    computes the same cuts from the same costs.  Returns uint16 [n, 4] rows of (tx, ty, cam, 0) per rank."""
+    tx_n, ty_n = (width + 7) // 8, (height + 7) // 8
+    n = ncams * ty_n * tx_n
+    w = np.ones(n) if costs is None else np.asarray(costs, np.float64).reshape(-1)
+    if w.size != n:
+        raise ValueError("costs must hold one weight per tile")
+    cum = np.concatenate([[0.0], np.cumsum(w)])
+    # cut k: the first tile index whose prefix weight reaches k/world of the total (monotone, cuts[0] = 0)
+    cuts = [0] + [int(np.searchsorted(cum, cum[-1] * k / world, side="left")) for k in range(1, world)] + [n]
+    cuts = np.maximum.accumulate(np.minimum(cuts, n))
+    idx = np.arange(n)
+    cam, rem = idx // (ty_n * tx_n), idx % (ty_n * tx_n)
+    ty, tx = rem // tx_n, rem % tx_n
+    rows = np.stack([tx, ty, cam, np.zeros_like(tx)], axis=1).astype(np.uint16)
+    return [rows[cuts[r]:cuts[r + 1]] for r in range(world)]
+
+
 def rank_views(views, world):
     """Views of every rank, round-robin (config 5 shards whole views over GPUs)."""
     return [list(range(r, views, world)) for r in range(world)]

@@ -145,6 +145,17 @@ class Renderer:
         check(lib().gvrt_get_option(self.h, _lib.OPTIONS[name], C.byref(v)), self.h)
         return int(v.value)
 
+    def tile_costs(self, width=None, height=None, ncams=1, ntiles=None):
+        """gvrt_read_tile_costs: the last cost-ordered launch's per-tile cost classes (c: ~2^(c/4) k cycles).
+        Full frame: uint8 [ncams, ceil(H/8), ceil(W/8)]; a caller tile list: ntiles=len(list), uint8 [ntiles]."""
+        if ntiles is None:
+            shape = (ncams, (height + 7) // 8, (width + 7) // 8)
+        else:
+            shape = (int(ntiles),)
+        out = np.zeros(shape, np.uint8)
+        check(lib().gvrt_read_tile_costs(self.h, out.ctypes.data, out.size), self.h)
+        return out
+
     def set_stats(self, on=True):
         check(lib().gvrt_set_stats(self.h, 1 if on else 0), self.h)
 

@@ -188,15 +188,36 @@ def rank_balance(args, r, gv, dist_mod, vi_all, pi, W, H, views, params, full_ms
     n = args.rank_balance
     dev = torch.device("cuda", 0)
     ms = []
+    layouts = {}
     if args.split == "tiles":
+        def time_parts(parts):
+            buf = torch.zeros((max(t.shape[0] for t in parts) * 64, 4), dtype=torch.uint8, device=dev)
+            out = []
+            for t in parts:
+                got = []
+                for _ in range(reps):
+                    r.render_device(vi_all[:16], pi, W, H, 1, params=params, tiles=t, rgba8_ptr=buf.data_ptr(),
+                                    packed=True)
+                    got.append(r.render_ms())
+                out.append(float(np.median(got[1:])))
+            return out
+
+        # the full frame's per-tile costs (two launches: the second is cost-ordered and records them again)
+        fbuf = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
+        for _ in range(2):
+            r.render_device(vi_all[:16], pi, W, H, 1, params=params, rgba8_ptr=fbuf.data_ptr())
+        costs = dist_mod.cost_weights(r.tile_costs(W, H))
+        alts = {"bands": dist_mod.band_tiles(W, H, n),
+                "cost_bands": dist_mod.band_tiles(W, H, n, costs=costs)}
         parts = dist_mod.rank_tiles(W, H, 1, n, block=8)
-        buf = torch.zeros((max(t.shape[0] for t in parts) * 64, 4), dtype=torch.uint8, device=dev)
-        for t in parts:
-            got = []
-            for _ in range(reps):
-                r.render_device(vi_all[:16], pi, W, H, 1, params=params, tiles=t, rgba8_ptr=buf.data_ptr(), packed=True)
-                got.append(r.render_ms())
-            ms.append(float(np.median(got[1:])))
+        ms = time_parts(parts)
+        for name, p in alts.items():
+            pm = time_parts(p)
+            est = [float(costs.reshape(-1)[(t[:, 1].astype(np.int64) * ((W + 7) // 8) + t[:, 0])].sum()) for t in p]
+            layouts[name] = {"tiles": [int(t.shape[0]) for t in p], "kernel_ms": [round(x, 4) for x in pm],
+                             "max_over_mean": round(max(pm) / float(np.mean(pm)), 4),
+                             "implied_efficiency": round(full_ms / (n * max(pm)), 4),
+                             "cost_max_over_mean_est": round(max(est) / float(np.mean(est)), 4)}
         what = f"{n} tile lists (64x64-pixel blocks round-robin), {parts[0].shape[0]}..{parts[-1].shape[0]} tiles each"
     else:
         vis = np.asarray(vi_all, np.float32).reshape(-1, 16)
@@ -223,6 +244,8 @@ def rank_balance(args, r, gv, dist_mod, vi_all, pi, W, H, views, params, full_ms
         extra = {"view_ms": [round(x, 4) for x in view_costs],
                  "round_robin_max_over_mean_est": round(max(rrc) / float(np.mean(rrc)), 4),
                  "balanced_max_over_mean_est": round(max(bc) / float(np.mean(bc)), 4)}
+    if layouts:
+        extra["other_layouts"] = layouts
     return {**extra, "ranks": n, "parts": what, "kernel_ms": [round(x, 4) for x in ms], "max_over_mean": round(mx / mean, 4),
             "full_kernel_ms": round(full_ms, 4), "implied_efficiency": round(full_ms / (n * mx), 4),
             "note": "each part alone on one GPU with its own cost-ordered dispatch; median of the ordered launches"}

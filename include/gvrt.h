@@ -277,6 +277,13 @@ gvrt_status gvrt_unpack_tiles_rgba8(gvrt_handle h, const void* packed, const gvr
                                     uint64_t ntiles, uint32_t width, uint32_t height, uint32_t ncams,
                                     void* frame);
 
+/* Per-tile cost classes of the last cost-ordered launch (GVRT_OPT_TILE_ORDER): class c means the tile's wave
+ * ran about 2^(c/4) x 1024 cycles (0..63).  A full-frame launch fills out[(cam * ceil(H/8) + ty) * ceil(W/8) + tx];
+ * a caller tile list fills out[i] for list entry i.  n must be that tile count.  Waits for queued launches.
+ * GVRT_ERR_STATE when no ordered launch has run at this size.  The multi-GPU tile split uses it to cut the
+ * frame into parts of equal cost; the reference has no equivalent (one GPU, one dispatch). */
+gvrt_status gvrt_read_tile_costs(gvrt_handle h, uint8_t* out, uint64_t n);
+
 /* --------------------------------------------------------------------------------------- */
 /* Host-side loader: vk3DGRT::PLYLoader::loadPLYModel (base/Vulkan3DGRTModel.cpp:7-125).
  * Allocates host arrays owned by the returned object; free with gvrt_ply_free. */

@@ -558,3 +558,34 @@ def test_tuning_options_change_no_pixel(gv, config1, option):
             r.set_option(option, 9 if option == "order_spread" else 2)
     for a, b in zip(ref, got):
         np.testing.assert_array_equal(a, b)
+
+
+def test_read_tile_costs(gv, config1):
+    """gvrt_read_tile_costs: the last ordered launch's per-tile cost classes, full frame in [cam][ty][tx] layout
+    (the frame's costly tiles are the ones the scene covers) and per list entry for a caller tile list; refused
+    before any ordered launch and for a wrong count."""
+    W, H = 200, 136
+    vi, pi = gv.scene.config1_camera(W, H)
+    with gv.Renderer(0) as r:
+        r.prepare(config1)
+        with pytest.raises(gv.GvrtError):
+            r.tile_costs(W, H)
+        r.render(vi, pi, W, H)
+        c = r.tile_costs(W, H)
+        assert c.shape == (1, 17, 25) and c.dtype == np.uint8 and int(c.max()) < 64
+        hc = r.render(vi, pi, W, H, hit_counts=True)["hit_counts"].reshape(H, W)
+        # tiles with many composited hits cost more than empty ones
+        per_tile = np.zeros((17, 25))
+        for ty in range(17):
+            for tx in range(25):
+                per_tile[ty, tx] = hc[ty * 8:ty * 8 + 8, tx * 8:tx * 8 + 8].sum()
+        busy, empty = per_tile > np.percentile(per_tile, 90), per_tile == 0
+        if empty.any():
+            assert c[0][busy].mean() > c[0][empty].mean()
+        with pytest.raises(gv.GvrtError):
+            lib_n = c.size + 1
+            r.tile_costs(ntiles=lib_n)
+        tiles = gv.tiles_for_rank(W, H, 1, 0, 2, block=2)
+        r.render(vi, pi, W, H, tiles=tiles, packed=True)
+        cl = r.tile_costs(ntiles=len(tiles))
+        assert cl.shape == (len(tiles),) and int(cl.max()) < 64
