@@ -33,25 +33,29 @@ def cost_weights(classes):
     return np.exp2(np.asarray(classes, np.float64) / 4.0)
 
 
-def band_tiles(width, height, world, costs=None, ncams=1):
-    """Contiguous parts of the row-major tile order of each camera, one per rank: equal tile counts, or equal
-    summed cost when `costs` (per-tile weights [ncams, ty, tx], e.g. cost_weights of a previous frame's classes)
-    is given.  A part is a compact screen band (its tiles share BVH nodes and records in that GPU's caches),
-    where the 64x64-block round-robin of rank_tiles scatters each part over the whole frame.  Every rank
-    computes the same cuts from the same costs.  Returns uint16 [n, 4] rows of (tx, ty, cam, 0) per rank."""
+def band_tiles(width, height, world, costs=None, ncams=1, block=8):
+    """Contiguous parts of the frame, one per rank: the tiles in the order of rank_tiles' blocks (block x block
+    tiles, blocks row-major, tiles row-major inside a block) cut into `world` runs of equal tile count, or of
+    equal summed cost when `costs` (per-tile weights [ncams, ty, tx], e.g. cost_weights of a previous frame's
+    classes) is given.  A part is then a band of block rows (its tiles share BVH nodes and records in that
+    GPU's caches, and the block order keeps the XCD dealing of each cost class compact), where the block
+    round-robin of rank_tiles scatters each part over the whole frame.  world = 1 gives rank_tiles' list.
+    Every rank computes the same cuts from the same costs.  Returns uint16 [n, 4] rows of (tx, ty, cam, 0)."""
+    rows = tiles_for_rank(width, height, ncams, 0, 1, block).astype(np.int64)
     tx_n, ty_n = (width + 7) // 8, (height + 7) // 8
-    n = ncams * ty_n * tx_n
-    w = np.ones(n) if costs is None else np.asarray(costs, np.float64).reshape(-1)
-    if w.size != n:
-        raise ValueError("costs must hold one weight per tile")
+    n = rows.shape[0]
+    if costs is None:
+        w = np.ones(n)
+    else:
+        c = np.asarray(costs, np.float64)
+        if c.size != ncams * ty_n * tx_n:
+            raise ValueError("costs must hold one weight per tile")
+        w = c.reshape(ncams, ty_n, tx_n)[rows[:, 2], rows[:, 1], rows[:, 0]]
     cum = np.concatenate([[0.0], np.cumsum(w)])
-    # cut k: the first tile index whose prefix weight reaches k/world of the total (monotone, cuts[0] = 0)
+    # cut k: the first list position whose prefix weight reaches k/world of the total
     cuts = [0] + [int(np.searchsorted(cum, cum[-1] * k / world, side="left")) for k in range(1, world)] + [n]
     cuts = np.maximum.accumulate(np.minimum(cuts, n))
-    idx = np.arange(n)
-    cam, rem = idx // (ty_n * tx_n), idx % (ty_n * tx_n)
-    ty, tx = rem // tx_n, rem % tx_n
-    rows = np.stack([tx, ty, cam, np.zeros_like(tx)], axis=1).astype(np.uint16)
+    rows = rows.astype(np.uint16)
     return [rows[cuts[r]:cuts[r + 1]] for r in range(world)]
 
 

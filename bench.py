@@ -65,6 +65,10 @@ def parse():
     ap.add_argument("--exchange", action="store_true",
                     help="run the multi-GPU frame-exchange path even with one rank (torch.distributed.run "
                          "--nproc-per-node 1: rehearses the N-rank step on one GPU)")
+    ap.add_argument("--tile-layout", default="cost-bands", choices=["cost-bands", "bands", "blocks"],
+                    help="tile split: contiguous row-major bands of equal cost (rank 0 measures the per-tile costs of "
+                         "the full frame once at set-up and broadcasts them), bands of equal tile count, or 64x64-pixel "
+                         "blocks round-robin")
     ap.add_argument("--camera-path", default="static", choices=["static", "orbit"],
                     help="static: every frame renders the config camera (the headline); orbit: the camera's azimuth "
                          "advances by --orbit-step degrees per frame (a moving camera: the reference's frame loop "
@@ -166,6 +170,23 @@ def pmc_passes(args):
     return out
 
 
+def tile_cost_calibration(r, vi, pi, W, H, params):
+    """Per-tile cost classes of the full frame (gvrt_read_tile_costs after two launches, the second cost-ordered),
+    for the cost-weighted band split; before the timed region."""
+    import torch
+    buf = torch.zeros((H, W, 4), dtype=torch.uint8, device=torch.device("cuda", torch.cuda.current_device()))
+    for _ in range(2):
+        r.render_device(vi, pi, W, H, 1, params=params, rgba8_ptr=buf.data_ptr())
+    return r.tile_costs(W, H)
+
+
+def split_tiles(dist_mod, layout, W, H, world, classes=None):
+    """Every rank's tile list for the tile split (--tile-layout)."""
+    if layout == "blocks":
+        return dist_mod.rank_tiles(W, H, 1, world, block=8)
+    return dist_mod.band_tiles(W, H, world, costs=dist_mod.cost_weights(classes) if layout == "cost-bands" else None)
+
+
 def view_cost_calibration(r, vis, pi, W, H, params, reps=2):
     """Kernel ms of each view of the rig rendered alone (the last of `reps` launches: cost-ordered)."""
     import torch
@@ -206,10 +227,15 @@ def rank_balance(args, r, gv, dist_mod, vi_all, pi, W, H, views, params, full_ms
         fbuf = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
         for _ in range(2):
             r.render_device(vi_all[:16], pi, W, H, 1, params=params, rgba8_ptr=fbuf.data_ptr())
-        costs = dist_mod.cost_weights(r.tile_costs(W, H))
-        alts = {"bands": dist_mod.band_tiles(W, H, n),
-                "cost_bands": dist_mod.band_tiles(W, H, n, costs=costs)}
-        parts = dist_mod.rank_tiles(W, H, 1, n, block=8)
+        classes = r.tile_costs(W, H)
+        costs = dist_mod.cost_weights(classes)
+        alts = {k: split_tiles(dist_mod, k, W, H, n, classes) for k in ("cost-bands", "bands", "blocks")
+                if k != args.tile_layout}
+        parts = split_tiles(dist_mod, args.tile_layout, W, H, n, classes)
+        # every layout timed twice, in turn, and the second pass kept (the first parts timed in a process ran
+        # up to 10 % slower, whichever layout they belonged to)
+        for lay in [parts, *alts.values()]:
+            time_parts(lay)
         ms = time_parts(parts)
         for name, p in alts.items():
             pm = time_parts(p)
@@ -218,7 +244,8 @@ def rank_balance(args, r, gv, dist_mod, vi_all, pi, W, H, views, params, full_ms
                              "max_over_mean": round(max(pm) / float(np.mean(pm)), 4),
                              "implied_efficiency": round(full_ms / (n * max(pm)), 4),
                              "cost_max_over_mean_est": round(max(est) / float(np.mean(est)), 4)}
-        what = f"{n} tile lists (64x64-pixel blocks round-robin), {parts[0].shape[0]}..{parts[-1].shape[0]} tiles each"
+        what = (f"{n} tile lists, layout {args.tile_layout}, "
+                f"{min(t.shape[0] for t in parts)}..{max(t.shape[0] for t in parts)} tiles each")
     else:
         vis = np.asarray(vi_all, np.float32).reshape(-1, 16)
         rr = dist_mod.rank_views(views, n)
@@ -342,7 +369,17 @@ def main():
     else:
         frame_vi = [np.ascontiguousarray(v[0]) for v, _ in rigs]
         ncams = 1
-        all_tiles = dist_mod.rank_tiles(W, H, 1, world, block=8)
+        classes = None
+        if args.tile_layout == "cost-bands":
+            # the frame's tiles differ in cost (4x on bicycle): rank 0 measures them once, every rank gets the
+            # classes (one broadcast at set-up, not per frame) and computes the same band cuts
+            classes = (tile_cost_calibration(r, frame_vi[0], pi, W, H, params) if rank == 0
+                       else np.zeros((1, (H + 7) // 8, (W + 7) // 8), np.uint8))
+            if distributed:
+                t = torch.from_numpy(classes).to(dev)
+                dist.broadcast(t, src=0)
+                classes = t.cpu().numpy()
+        all_tiles = split_tiles(dist_mod, args.tile_layout, W, H, world, classes)
         tiles = all_tiles[rank]
         rays_per_rank = int(tiles.shape[0]) * 64
         part_sizes, item_shape = [t.shape[0] * 64 for t in all_tiles], (4,)
@@ -580,6 +617,7 @@ def main():
                                    f"ray-query variant, {args.mode} k-buffer",
                        "gaussians": n_input, "survivors": m, "width": W, "height": H,
                        "views": views, "split": args.split, "parallelism": f"{args.split}{world}",
+                       **({"tile_layout": args.tile_layout} if args.split == "tiles" else {}),
                        "dispatch": "tiles costliest-first by the previous frame's per-tile cost, each cost class "
                                    "dealt to the 8 XCDs in contiguous chunks (handle options tile_order=0: supertile order; "
                                    "tile_xcd=0: no dealing)",

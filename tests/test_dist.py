@@ -198,16 +198,19 @@ def test_balanced_views_equal_counts_and_lpt(gv):
 
 @pytest.mark.parametrize("W,H,world", [(3840, 2160, 8), (1920, 1080, 3), (100, 60, 2), (8, 8, 4)])
 def test_band_tiles_cover_the_frame_in_contiguous_parts(gv, W, H, world):
-    """dist.band_tiles: every tile exactly once, each rank a contiguous run of the row-major tile order, equal
-    counts without costs and (near) equal summed cost with them."""
+    """dist.band_tiles: every tile exactly once, each rank a contiguous run of rank_tiles' block order (world 1:
+    rank_tiles' own list), equal counts without costs and (near) equal summed cost with them."""
     dist = importlib.import_module("3dgvrt_lightfield_amd.dist")
     tx_n, ty_n = (W + 7) // 8, (H + 7) // 8
+    order = dist.rank_tiles(W, H, 1, 1)[0].astype(np.int64)
+    order = order[:, 1] * tx_n + order[:, 0]
+    np.testing.assert_array_equal(dist.band_tiles(W, H, 1)[0], dist.rank_tiles(W, H, 1, 1)[0])
     for costs in (None, np.random.default_rng(world).random((1, ty_n, tx_n)) * 3 + 0.1):
         parts = dist.band_tiles(W, H, world, costs=costs)
         assert len(parts) == world
         lin = [p[:, 1].astype(np.int64) * tx_n + p[:, 0] for p in parts]
         allt = np.concatenate(lin)
-        np.testing.assert_array_equal(allt, np.arange(tx_n * ty_n))  # in order, each once
+        np.testing.assert_array_equal(allt, order)  # the block order, cut in runs: each tile once
         w = np.ones(tx_n * ty_n) if costs is None else costs.reshape(-1)
         sums = [w[l].sum() for l in lin]
         if tx_n * ty_n >= 100 * world:
