@@ -28,9 +28,15 @@ def rank_tiles(width, height, ncams, world, block=8):
     return [tiles_for_rank(width, height, ncams, r, world, block) for r in range(world)]
 
 
+# 2^(k/4), k = 0..3, as exact decimal literals: cost_weights is 2^(c div 4) x QUARTER_OCTAVES[c mod 4], bit for
+# bit the same doubles as the C++ host's (gvrt_rccl.cpp), so both compute the same band cuts
+QUARTER_OCTAVES = (1.0, 1.189207115002721, 1.4142135623730951, 1.681792830507429)
+
+
 def cost_weights(classes):
     """Relative cost of a tile from its class (gvrt_read_tile_costs: 4 classes per octave of wave cycles)."""
-    return np.exp2(np.asarray(classes, np.float64) / 4.0)
+    c = np.asarray(classes, np.int64)
+    return np.ldexp(np.asarray(QUARTER_OCTAVES, np.float64)[c & 3], c >> 2)
 
 
 def band_tiles(width, height, world, costs=None, ncams=1, block=8):

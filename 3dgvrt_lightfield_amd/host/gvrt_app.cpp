@@ -8,13 +8,14 @@
 //   gvrt_app lightfield --ply P [--width 180 --height 180] --out D          (computeGaussianLightField)
 //   gvrt_app hitcounts  --ply P [...] --out D                                (printRayHitCounts)
 //   gvrt_app bench      --ply P [--duration 10 --warmup 1 --frametimes] --out D   (vks::Benchmark, fps.txt)
-//   gvrt_app split      --ply P --rank R --world N --id-file F [--frames K] --out D
+//   gvrt_app split      --ply P --rank R --world N --id-file F [--frames K] [--layout cost-bands|blocks] --out D
 //                       (one process per GPU: this rank's tiles of each frame, RCCL gather to rank 0, gvrt_rccl.h;
 //                        rank 0 writes split_frame.png, checks it against a one-GPU render of the same frame and
 //                        prints one JSON line)
 //   gvrt_app cameras    [--width W --height H] [--transforms T]   (prints the camera matrices; no GPU)
 //   gvrt_app png        OUT.png                                   (writes a test pattern; no GPU)
-//   gvrt_app tiles      --rank R --world N [--width W --height H]  (this rank's split tile list; no GPU)
+//   gvrt_app tiles      --rank R --world N [--width W --height H] [--layout blocks|bands --costs F]
+//                       (this rank's split tile list; F: raw uint8 cost classes [ty][tx]; no GPU)
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -112,9 +113,23 @@ int main(int argc, char** argv) {
             return write_png(out, img.data(), W, H) ? 0 : 1;
         }
         if (a.cmd == "tiles") {  // host-only: the tile split of gvrt_rccl.h, "tx ty cam" per line
-            for (const gvrt_tile& t : gvrt_host::rank_tiles(W, H, 1, std::atoi(a.get("rank", "0").c_str()),
-                                                             std::atoi(a.get("world", "1").c_str())))
-                std::printf("%u %u %u\n", t.tx, t.ty, t.cam);
+            const int rank = std::atoi(a.get("rank", "0").c_str()), world = std::atoi(a.get("world", "1").c_str());
+            std::vector<gvrt_tile> tl;
+            if (a.get("layout", "blocks") == "bands") {
+                std::vector<uint8_t> cls;
+                if (a.has("costs")) {
+                    FILE* f = std::fopen(a.get("costs").c_str(), "rb");
+                    if (!f) throw std::runtime_error("cannot open " + a.get("costs"));
+                    cls.resize((size_t)((W + 7) / 8) * ((H + 7) / 8));
+                    const size_t got = std::fread(cls.data(), 1, cls.size(), f);
+                    std::fclose(f);
+                    if (got != cls.size()) throw std::runtime_error("cost file: one class byte per tile");
+                }
+                tl = gvrt_host::band_tiles(W, H, world, cls.empty() ? nullptr : cls.data())[rank];
+            } else {
+                tl = gvrt_host::rank_tiles(W, H, 1, rank, world);
+            }
+            for (const gvrt_tile& t : tl) std::printf("%u %u %u\n", t.tx, t.ty, t.cam);
             return 0;
         }
         if (a.cmd == "cameras") {  // host-only: the camera matrices the C-ABI receives (uint32 bit patterns)
@@ -202,7 +217,9 @@ int main(int argc, char** argv) {
             std::vector<uint8_t> got((size_t)4 * W * H), one((size_t)4 * W * H);
             double ms = 0.0;
             {
-                gvrt_host::SplitFrame sf(app, rank, world, id, W, H);
+                const auto layout = a.get("layout", "cost-bands") == "blocks" ? gvrt_host::SplitFrame::BLOCKS
+                                                                              : gvrt_host::SplitFrame::COST_BANDS;
+                gvrt_host::SplitFrame sf(app, rank, world, id, W, H, layout);
                 if (sf.status() != GVRT_OK) throw std::runtime_error("SplitFrame: " + sf.error());
                 if (sf.draw(frame) != GVRT_OK || sf.sync() != GVRT_OK) throw std::runtime_error(sf.error());  // warm-up
                 const auto t0 = std::chrono::steady_clock::now();

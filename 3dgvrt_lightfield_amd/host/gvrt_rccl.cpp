@@ -4,7 +4,9 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <fstream>
 #include <thread>
@@ -26,6 +28,35 @@ std::vector<gvrt_tile> rank_tiles(uint32_t width, uint32_t height, uint32_t ncam
                     for (uint32_t tx = bx * block; tx < std::min((bx + 1) * block, tx_n); ++tx)
                         out.push_back(gvrt_tile{(uint16_t)tx, (uint16_t)ty, (uint16_t)c, 0});
             }
+    return out;
+}
+
+std::vector<std::vector<gvrt_tile>> band_tiles(uint32_t width, uint32_t height, int world, const uint8_t* classes,
+                                               uint32_t block) {
+    // dist.band_tiles: prefix sums of the weights in block order, cut k at the first position whose prefix reaches
+    // k/world of the total (numpy searchsorted, side left)
+    static const double quarter[4] = {1.0, 1.189207115002721, 1.4142135623730951, 1.681792830507429};
+    const std::vector<gvrt_tile> order = rank_tiles(width, height, 1, 0, 1, block);
+    const uint32_t tx_n = (width + 7) / 8;
+    const size_t n = order.size();
+    std::vector<double> cum(n + 1, 0.0);
+    for (size_t i = 0; i < n; ++i) {
+        double w = 1.0;
+        if (classes) {
+            const uint32_t c = classes[(size_t)order[i].ty * tx_n + order[i].tx];
+            w = std::ldexp(quarter[c & 3u], (int)(c >> 2));
+        }
+        cum[i + 1] = cum[i] + w;
+    }
+    std::vector<size_t> cuts(world + 1, 0);
+    cuts[world] = n;
+    for (int k = 1; k < world; ++k) {
+        const double target = cum[n] * k / world;
+        cuts[k] = std::min(n, (size_t)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin()));
+        cuts[k] = std::max(cuts[k], cuts[k - 1]);
+    }
+    std::vector<std::vector<gvrt_tile>> out(world);
+    for (int r = 0; r < world; ++r) out[r].assign(order.begin() + cuts[r], order.begin() + cuts[r + 1]);
     return out;
 }
 
@@ -77,7 +108,39 @@ gvrt_status SplitFrame::rccl(ncclResult_t r, const char* what) {
     return fail(GVRT_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
-SplitFrame::SplitFrame(GvrtApp& app, int rank, int world, const ncclUniqueId& id, uint32_t width, uint32_t height)
+gvrt_status SplitFrame::cost_classes(std::vector<uint8_t>* classes) {
+    gvrt_handle h = app_.handle();
+    const uint64_t n = (uint64_t)((width_ + 7) / 8) * ((height_ + 7) / 8);
+    classes->assign(n, 0);
+    uint8_t* d = nullptr;
+    if (hipMalloc(&d, std::max<uint64_t>(n, (uint64_t)4 * width_ * height_)) != hipSuccess)
+        return fail(GVRT_ERR_OOM, "cost-class buffer");
+    gvrt_status s = GVRT_OK;
+    if (rank_ == 0) {
+        // the full frame twice: the second launch is cost-ordered and records every tile's class again
+        gvrt_image img{d, nullptr, nullptr, nullptr, 1, 0};
+        for (int k = 0; k < 2 && s == GVRT_OK; ++k)
+            if (gvrt_render_async(h, &app_.params, app_.uniformDataDynamic.viewInverse.data(),
+                                  app_.uniformDataDynamic.projInverse.data(), width_, height_, 1, nullptr, 0,
+                                  &img) != GVRT_OK ||
+                gvrt_sync(h) != GVRT_OK)
+                s = fail(GVRT_ERR_HIP, std::string("calibration render: ") + gvrt_last_error(h));
+        if (s == GVRT_OK && gvrt_read_tile_costs(h, classes->data(), n) != GVRT_OK)
+            s = fail(GVRT_ERR_HIP, std::string("gvrt_read_tile_costs: ") + gvrt_last_error(h));
+        if (s == GVRT_OK && hipMemcpy(d, classes->data(), n, hipMemcpyHostToDevice) != hipSuccess)
+            s = fail(GVRT_ERR_HIP, "class upload");
+    }
+    // one broadcast at set-up (not per frame): every rank cuts the same bands from the same classes
+    if (s == GVRT_OK) s = rccl(ncclBroadcast(d, d, n, ncclUint8, 0, comm_, stream_), "ncclBroadcast");
+    if (s == GVRT_OK && hipStreamSynchronize(stream_) != hipSuccess) s = fail(GVRT_ERR_HIP, "broadcast sync");
+    if (s == GVRT_OK && hipMemcpy(classes->data(), d, n, hipMemcpyDeviceToHost) != hipSuccess)
+        s = fail(GVRT_ERR_HIP, "class readback");
+    (void)hipFree(d);
+    return s;
+}
+
+SplitFrame::SplitFrame(GvrtApp& app, int rank, int world, const ncclUniqueId& id, uint32_t width, uint32_t height,
+                       Layout layout)
     : app_(app), rank_(rank), world_(world), width_(width), height_(height) {
     if (world < 1 || rank < 0 || rank >= world) {
         fail(GVRT_ERR_INVALID_ARG, "rank must be in [0, world)");
@@ -97,7 +160,13 @@ SplitFrame::SplitFrame(GvrtApp& app, int rank, int world, const ncclUniqueId& id
         fail(GVRT_ERR_HIP, std::string("gvrt_set_stream: ") + gvrt_last_error(app.handle()));
         return;
     }
-    for (int r = 0; r < world; ++r) all_tiles_.push_back(rank_tiles(width, height, 1, r, world));
+    if (layout == COST_BANDS) {
+        std::vector<uint8_t> classes;
+        if (cost_classes(&classes) != GVRT_OK) return;
+        all_tiles_ = band_tiles(width, height, world, classes.data());
+    } else {
+        for (int r = 0; r < world; ++r) all_tiles_.push_back(rank_tiles(width, height, 1, r, world));
+    }
     tiles_ = all_tiles_[rank];
     if (hipMalloc(&d_part_, std::max<size_t>(16, (size_t)tiles_.size() * 256)) != hipSuccess) {
         d_part_ = nullptr;

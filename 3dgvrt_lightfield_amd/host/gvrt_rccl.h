@@ -26,6 +26,12 @@ namespace gvrt_host {
 std::vector<gvrt_tile> rank_tiles(uint32_t width, uint32_t height, uint32_t ncams, int rank, int world,
                                   uint32_t block = 8);
 
+// Every rank's tile list for the cost-weighted band split (dist.band_tiles): the tiles in rank_tiles' block
+// order (world 1) cut into `world` runs of equal summed cost, a tile of class c weighing 2^(c/4) (classes:
+// gvrt_read_tile_costs of a full frame, [ty][tx]); classes == nullptr: runs of equal tile count.
+std::vector<std::vector<gvrt_tile>> band_tiles(uint32_t width, uint32_t height, int world, const uint8_t* classes,
+                                               uint32_t block = 8);
+
 // Rendezvous of the communicator: rank 0 creates the RCCL unique id and writes it to `path` (written to a
 // temporary name and renamed, so a reader never sees half a file); every other rank waits for the file (up to
 // timeout_s seconds).  Returns GVRT_OK or GVRT_ERR_RCCL / GVRT_ERR_IO with the text in *err.
@@ -34,8 +40,13 @@ gvrt_status rccl_rendezvous(const std::string& path, int rank, ncclUniqueId* id,
 
 class SplitFrame {
   public:
-    // ncclCommInitRank(world, id, rank) on the app's device; the app's handle then renders on this object's stream
-    SplitFrame(GvrtApp& app, int rank, int world, const ncclUniqueId& id, uint32_t width, uint32_t height);
+    enum Layout { BLOCKS = 0, COST_BANDS = 1 };
+    // ncclCommInitRank(world, id, rank) on the app's device; the app's handle then renders on this object's stream.
+    // COST_BANDS: rank 0 renders the app's current frame twice and reads its per-tile cost classes
+    // (gvrt_read_tile_costs), one ncclBroadcast hands them to every rank, and all cut the same bands (band_tiles);
+    // BLOCKS: 64x64-pixel blocks round-robin (rank_tiles)
+    SplitFrame(GvrtApp& app, int rank, int world, const ncclUniqueId& id, uint32_t width, uint32_t height,
+               Layout layout = COST_BANDS);
     ~SplitFrame();
     SplitFrame(const SplitFrame&) = delete;
     SplitFrame& operator=(const SplitFrame&) = delete;
@@ -56,6 +67,7 @@ class SplitFrame {
   private:
     gvrt_status fail(gvrt_status s, const std::string& m);
     gvrt_status rccl(ncclResult_t r, const char* what);
+    gvrt_status cost_classes(std::vector<uint8_t>* classes);  // rank 0 measures, every rank receives
 
     GvrtApp& app_;
     int rank_, world_;

@@ -116,11 +116,13 @@ def test_cpp_app_flows_match_python(gv, tmp_path):
     assert (out / "fps.txt").read_text().startswith("device,driverversion,duration (ms),frames,fps\n")
 
 
-def test_cpp_rccl_split_frame_one_rank(gv, tmp_path):
+@pytest.mark.parametrize("layout", ["cost-bands", "blocks"])
+def test_cpp_rccl_split_frame_one_rank(gv, tmp_path, layout):
     """The native multi-GPU path of the C++ host (host/gvrt_rccl.h SplitFrame: ncclCommInitRank, this rank's
     tiles rendered tile-packed, grouped ncclSend / ncclRecv to rank 0, gvrt_unpack_tiles_rgba8) with a one-rank
     communicator: rank 0 sends its part to itself through RCCL, and the gathered frame equals the one-GPU frame
-    byte for byte (the app checks and prints it)."""
+    byte for byte (the app checks and prints it).  cost-bands: rank 0's calibration renders, gvrt_read_tile_costs
+    and the ncclBroadcast of the classes run first."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     exe = os.path.join(root, "3dgvrt_lightfield_amd", "gvrt_app")
     ply = str(tmp_path / "scene.ply")
@@ -129,7 +131,7 @@ def test_cpp_rccl_split_frame_one_rank(gv, tmp_path):
     for W, H in ((256, 256), (200, 120)):
         r = subprocess.run([exe, "split", "--ply", ply, "--rank", "0", "--world", "1", "--id-file",
                             str(tmp_path / f"rccl_{W}.id"), "--frames", "4", "--camera", "config1", "--width", str(W),
-                            "--height", str(H), "--out", str(tmp_path / f"split_{W}")],
+                            "--height", str(H), "--layout", layout, "--out", str(tmp_path / f"split_{W}")],
                            capture_output=True, text=True, timeout=180,
                            env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
         assert r.returncode == 0, r.stderr[-2000:]

@@ -206,3 +206,22 @@ def test_cpp_split_tiles_match_python(gv, W, H, world):
         np.testing.assert_array_equal(got, ref)
         seen.extend(map(tuple, got))
     assert len(seen) == len(set(seen)) == ((W + 7) // 8) * ((H + 7) // 8)
+
+
+@pytest.mark.parametrize("W,H,world", [(3840, 2160, 8), (1920, 1080, 3), (100, 60, 2)])
+def test_cpp_cost_bands_match_python(gv, tmp_path, W, H, world):
+    """The C++ host's cost-weighted band split (gvrt_rccl.h band_tiles, SplitFrame::COST_BANDS) cuts the same
+    bands as the Python layer (dist.band_tiles over dist.cost_weights) from the same cost classes: the weights
+    are the same doubles on both sides (2^(c div 4) x an exact quarter-octave literal)."""
+    import importlib
+    dist = importlib.import_module("3dgvrt_lightfield_amd.dist")
+    tx_n, ty_n = (W + 7) // 8, (H + 7) // 8
+    cls = np.random.default_rng(W + world).integers(0, 64, size=(ty_n, tx_n), dtype=np.uint8)
+    f = tmp_path / "classes.bin"
+    f.write_bytes(cls.tobytes())
+    ref = dist.band_tiles(W, H, world, costs=dist.cost_weights(cls[None]))
+    for rank in range(world):
+        out = run("tiles", "--rank", str(rank), "--world", str(world), "--width", str(W), "--height", str(H),
+                  "--layout", "bands", "--costs", str(f))
+        got = np.array([[int(v) for v in l.split()] for l in out.splitlines()], np.int64).reshape(-1, 3)
+        np.testing.assert_array_equal(got, ref[rank].astype(np.int64)[:, :3])
