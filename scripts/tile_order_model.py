@@ -4,7 +4,7 @@ in supertile order, in true-cost order, and in the order of a footprint estimate
 sphere rasterised into tile counts by a 2D difference array); prints makespans over the balanced bound and the
 Spearman correlation of the estimate with the measured cost."""
 import numpy as np
-sys.path.insert(0, "/root/repo")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 gv = importlib.import_module("3dgvrt_lightfield_amd")
 d = np.load(sys.argv[1])
 SLOTS = 4096
