@@ -215,3 +215,24 @@ def test_band_tiles_cover_the_frame_in_contiguous_parts(gv, W, H, world):
         sums = [w[l].sum() for l in lin]
         if tx_n * ty_n >= 100 * world:
             assert max(sums) <= (1.0 + 0.01) * np.mean(sums) + w.max()
+
+
+@pytest.mark.parametrize("layout", ["cost-bands", "bands", "blocks"])
+def test_bench_tile_layouts_cover_the_frame(gv, layout):
+    """bench.py --tile-layout: every layout gives every 4K tile to exactly one of 8 ranks; cost bands from a
+    cost-class map balance the summed cost (the split bench.py's tile branch and --rank-balance use)."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)  # no GPU work at import
+    dist = importlib.import_module("3dgvrt_lightfield_amd.dist")
+    W, H, world = 3840, 2160, 8
+    cls = np.random.default_rng(5).integers(0, 40, size=(1, 270, 480), dtype=np.uint8)
+    parts = bench.split_tiles(dist, layout, W, H, world, cls)
+    lin = np.concatenate([p[:, 1].astype(np.int64) * 480 + p[:, 0] for p in parts])
+    assert np.array_equal(np.sort(lin), np.arange(480 * 270))
+    if layout == "cost-bands":
+        w = dist.cost_weights(cls).reshape(-1)
+        sums = [w[p[:, 1].astype(np.int64) * 480 + p[:, 0]].sum() for p in parts]
+        assert max(sums) <= 1.001 * np.mean(sums) + w.max()
