@@ -661,17 +661,7 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                             const float hk =
                                 ADAPTIVE ? kernel_scale(rec.density, a.kmin, a.kopts, a.kdeg) * SQRT3 : a.kernel_h;
                             float tn, tf;
-#ifdef GVRT_EXP_NOCLIP
-                            {  // timing probe only: sphere interval around the closest approach (wrong image)
-                                const float l2i = __builtin_amdgcn_rcpf(l2);
-                                const float tm = -(ok.x * dk.x + ok.y * dk.y + ok.z * dk.z) * l2i;
-                                const float hw = hk * __builtin_amdgcn_sqrtf(l2i) * 0.8f;
-                                tn = tm - hw;
-                                tf = tm + hw;
-                            }
-#else
                             ico_clip(ok, dk, hk, tn, tf);
-#endif
                             if (tn <= tf) {
                                 const float al = acc ? galpha : -1.0f;
                                 // (an inclusive tmin exists only in LITERAL mode: the API refuses it otherwise)
