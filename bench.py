@@ -572,6 +572,20 @@ def main():
                              "frac_beyond_1e-4_off_threshold": float((d[~amb] > 1e-4).mean()) if (~amb).any() else 0.0,
                              "frac_beyond_1e-4_all": float((d > 1e-4).mean())}
 
+        # the host-buffer boundary (gvrt_render with host pointers: the frame staged in the handle's scratch and
+        # copied over PCIe, the call returns when the host holds it): rgba8 of the same frame, not the bench value
+        host_out = None
+        if world == 1 and args.split == "views" and ncams == 1:
+            for _ in range(2):
+                r.render(frame_vi[0], pi, W, H, 1, params=params, rgba32f=False)
+            reps = 10
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                r.render(frame_vi[0], pi, W, H, 1, params=params, rgba32f=False)
+            hms = (time.perf_counter() - t0) * 1e3 / reps
+            host_out = {"ms_per_frame": round(hms, 4), "mrays_per_s": round(W * H / hms / 1e3, 1),
+                        "note": "gvrt_render into host rgba8 (staged + D2H copy over PCIe, synchronous), 10 frames"}
+
         # moving camera: the same views rendered as static frames (each view twice in a row, the second launch
         # ordered by its own costs), so the moving-camera penalty is measured on equal work
         orbit_static = None
@@ -644,6 +658,8 @@ def main():
             result["rank_balance"] = balance
         if orbit_static:
             result["orbit_same_views_static"] = orbit_static
+        if host_out:
+            result["host_output_pcie"] = host_out
         if lit_stats:
             result["reference_counters"] = {"crossings_per_ray": lit_stats["crossings"] / (W * H),
                                             "accepted_per_ray": lit_stats["accepted"] / (W * H),
