@@ -1,7 +1,7 @@
 """Full-size SURVEY §8d configurations 3-5 and the dense stand-in on the GPU: size-independent properties plus
-the oracle over the whole frame (garden) or a 1/64 strided ray sample (truck 4K: 130 k rays, the light field:
-518 k of its 33.2 M rays, the dense stand-in: 32 k rays, whose ~150 crossings per ray cost the oracle ~14 min
-of CPU per full frame).  The oracle restates the reference's loop per ray, so a strided sample is a valid
+the oracle over the whole frame (garden) or a strided ray sample (the dense stand-in: every 8th ray, 259 k,
+since its ~10 LITERAL rounds of ~150 crossings per ray cost the oracle ~10 min per frame on 16 threads; truck
+4K: every 64th, 130 k rays; the light field: every 64th, 518 k of its 33.2 M rays).  The oracle restates the reference's loop per ray, so a strided sample is a valid
 sample.  Tolerances and the on-threshold accounting as in test_gpu_parity.py (every compared ray is bounded;
 on-threshold fractions capped near their measured values); tile / view splits are checked bit for bit.
 
@@ -104,14 +104,16 @@ def test_lightfield_grid_16_views(gv, O):
 
 def test_dense_standin(gv, O):
     """The dense stand-in (scene.dense_standin: ~150 crossings, ~79 accepted, ~10 LITERAL rounds per ray):
-    FAST and LITERAL vs the oracle on a strided subset, LITERAL counters vs the oracle's on that subset."""
+    FAST and LITERAL vs the oracle on every 8th ray of the 1080p frame (259 k rays; the oracle's ~10 LITERAL
+    rounds of ~150 crossings per ray make the whole frame take ~10 min on the GPU box's 16 threads, too long for
+    one test), FAST's accepted-hit counts vs the oracle's on every off-threshold ray."""
     splats, W, H, _ = _scene(gv, "dense")
     vi, pi = gv.scene.mipnerf_camera(W, H)
     with gv.Renderer(0) as r:
         m = r.prepare(splats)
         fast = r.render(vi, pi, W, H, hit_counts=True)
         lit = r.render(vi, pi, W, H, mode=gv.MODE_LITERAL)
-    m_ref, sub, ref = _oracle_subset(O, splats, vi, pi, W, H, stride=64)
+    m_ref, sub, ref = _oracle_subset(O, splats, vi, pi, W, H, stride=8)
     assert m_ref == m
     st = ref["stats"].reshape(-1, 3)
     assert st[:, 0].mean() > 140, st.mean(axis=0)  # the workload is what it claims to be
@@ -123,4 +125,4 @@ def test_dense_standin(gv, O):
     _cmp_images(lit["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.08)
     amb = O.ambiguous(ref["margin"])
     assert (fast["hit_counts"].reshape(-1)[idx] != st[:, 1])[~amb].sum() == 0
-    record_parity("dense", stride=64, **parity_figures(O, gv, fast["rgba32f"].reshape(-1, 4)[idx], ref))
+    record_parity("dense", stride=8, **parity_figures(O, gv, fast["rgba32f"].reshape(-1, 4)[idx], ref))
