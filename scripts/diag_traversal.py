@@ -1,7 +1,7 @@
 """Traversal diagnostics of the render kernel on a bench scene (stats-enabled renders).
 
 python scripts/diag_traversal.py [config] [kbuffer depths...]
-DIAG_OPTS="frontier=1,tile_order=0" sets handle options (gvrt_set_option) first.
+DIAG_OPTS="octant_nodes=0,tile_order=0" sets handle options (gvrt_set_option) first.
 """
 import importlib
 import json

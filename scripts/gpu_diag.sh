@@ -1,4 +1,4 @@
-# Traversal diagnostics (STATS counters + phase cycles): CFGS="bicycle dense" KS="24" OPTS_LIST="frontier=0 frontier=1"
+# Traversal diagnostics (STATS counters + phase cycles): CFGS="bicycle dense" KS="24" OPTS_LIST="none octant_nodes=0"
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/diag

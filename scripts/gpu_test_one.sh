@@ -1,4 +1,4 @@
-# Run a subset of the GPU tests: TESTS="tests/test_gpu_sah.py" [KEXPR="frontier or digest"] bash scripts/gpu_test_one.sh
+# Run a subset of the GPU tests: TESTS="tests/test_gpu_sah.py" [KEXPR="options or digest"] bash scripts/gpu_test_one.sh
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
