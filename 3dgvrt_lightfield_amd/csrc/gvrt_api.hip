@@ -604,11 +604,16 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
     if (c->n_leaves >= (1ull << 26) || c->n_nodes4 >= (1ull << 25))
         return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "more than 2^26 BVH leaves or 2^25 nodes (32-bit record offsets)");
     // cameras: uploaded only when they changed, into the next slot of the device ring, so that a moving camera
-    // costs no host round trip per frame (the slot's previous reader has long finished: its event is waited for
-    // only if the queue is CAM_RING frames deep)
+    // costs no host round trip per frame.  The outgoing slot's event is recorded when the camera changes (after
+    // every queued launch that read it), so a static camera records none; a slot's event is waited for only when
+    // the ring comes round to it with its readers still queued (CAM_RING camera changes deep)
     if ((s = ensure_cameras(c, ncams))) return s;
     if (!c->cam_valid || c->h_viewinv.size() != 16ull * ncams ||
         std::memcmp(c->h_viewinv.data(), view_inverse, 64ull * ncams) != 0) {
+        if (c->cam_valid) {
+            GVRT_HIP(c, hipEventRecord(c->cam_ev[c->cam_slot], c->stream));
+            c->cam_ev_live[c->cam_slot] = true;
+        }
         const uint32_t slot = (c->cam_slot + 1) % gvrt_context::CAM_RING;
         if (c->cam_ev_live[slot]) GVRT_HIP(c, hipEventSynchronize(c->cam_ev[slot]));
         float* src = c->h_viewinv_pin + slot * c->cam_stride;
@@ -748,22 +753,14 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
             }
         }
         hipEvent_t e0 = c->async_ev[2 * c->async_pending], e1 = c->async_ev[2 * c->async_pending + 1];
-        GVRT_HIP(c, hipEventRecord(e0, c->stream));
-        if ((s = gvrt_launch_render_mode(c, a, nwork, p->mode == GVRT_MODE_LITERAL))) return s;
-        GVRT_HIP(c, hipEventRecord(e1, c->stream));
-        GVRT_HIP(c, hipEventRecord(c->cam_ev[c->cam_slot], c->stream));
-        c->cam_ev_live[c->cam_slot] = true;
+        if ((s = gvrt_launch_render_mode(c, a, nwork, p->mode == GVRT_MODE_LITERAL, e0, e1))) return s;
         if (ordered && (s = gvrt_launch_tile_order(c, a.tiles, std::min(ord_radius, 8)))) return s;
         ++c->async_pending;
         c->stats.rays = (tiles || out->packed) ? nwork * 64 : total_tiles * 64;
         return GVRT_OK;
     }
     if ((c->async_pending || c->async_drained) && (s = finish_async(c))) return s;
-    GVRT_HIP(c, hipEventRecord(c->ev0, c->stream));
-    if ((s = gvrt_launch_render_mode(c, a, nwork, p->mode == GVRT_MODE_LITERAL))) return s;
-    GVRT_HIP(c, hipEventRecord(c->ev1, c->stream));
-    GVRT_HIP(c, hipEventRecord(c->cam_ev[c->cam_slot], c->stream));
-    c->cam_ev_live[c->cam_slot] = true;
+    if ((s = gvrt_launch_render_mode(c, a, nwork, p->mode == GVRT_MODE_LITERAL, c->ev0, c->ev1))) return s;
     if (ordered && (s = gvrt_launch_tile_order(c, a.tiles, std::min(ord_radius, 8)))) return s;
     if (!out->device_ptrs) {
         if (b32) GVRT_HIP(c, hipMemcpyAsync(out->rgba32f, a.rgba32f, b32, hipMemcpyDeviceToHost, c->stream));

@@ -145,7 +145,9 @@ gvrt_status gvrt_ploc_build(gvrt_context* c, uint32_t m, const float* leaf_boxes
 gvrt_status gvrt_sah_build_device(gvrt_context* c, uint64_t m, const float* lboxes, gvrt::BvhNode* nodes,
                                   gvrt::Bvh4Node* out4, uint32_t* depth_out, uint64_t* n4_out, uint32_t* depth4_out);
 // gvrt_render.hip
-gvrt_status gvrt_launch_render_mode(gvrt_context* c, const gvrt::RenderArgs& a, uint64_t nwaves, bool literal);
+// the render launch; ev_start / ev_stop are recorded at the kernel's start and end (its kernel time)
+gvrt_status gvrt_launch_render_mode(gvrt_context* c, const gvrt::RenderArgs& a, uint64_t nwaves, bool literal,
+                                    hipEvent_t ev_start, hipEvent_t ev_stop);
 // codes: the tile list the order is over (cam << 24 | ty << 12 | tx); radius > 0: classes spread by a max filter
 gvrt_status gvrt_launch_tile_order(gvrt_context* c, const uint32_t* codes, int radius);
 // record preparation: op 0 save leaf positions, 1 write kernel-frame origins for o, 2 restore positions

@@ -28,6 +28,8 @@
 // (16 per trace, `last` advanced by rejected hits too).  FAST = only accepted crossings enter the
 // k-buffer; with an exclusive tmin the composited sequence, and therefore the image, is the
 // same (rejected crossings only ever advanced `last`), while far fewer rounds are needed.
+#include <hip/hip_ext.h>
+
 #include "gvrt_internal.h"
 
 using namespace gvrt;
@@ -908,21 +910,32 @@ __global__ __launch_bounds__(256) void k_unpack(const uint32_t* __restrict__ pac
 
 }  // namespace
 
-gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64_t nwaves, bool literal) {
+gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64_t nwaves, bool literal,
+                                     hipEvent_t ev_start, hipEvent_t ev_stop) {
     uint64_t blocks = nwaves;
     if (!a.tiles)
         blocks = (uint64_t)((a.tiles_x + ST_W - 1) / ST_W) * ((a.tiles_y + ST_H - 1) / ST_H) * (ST_W * ST_H) * a.ncams;
-    if (nwaves == 0 || blocks == 0) return GVRT_OK;
+    if (nwaves == 0 || blocks == 0) {
+        GVRT_HIP(c, hipEventRecord(ev_start, c->stream));
+        GVRT_HIP(c, hipEventRecord(ev_stop, c->stream));
+        return GVRT_OK;
+    }
     if (blocks > 0x7FFFFFFFull) return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "too many tiles");
     const bool adaptive = (a.kopts & 1u) != 0;
     const dim3 g((unsigned)blocks), b(64);
     // every pointer is its own __restrict__ argument: the uniform node / record loads can then be
     // proven unclobbered by the output stores and are emitted as scalar (s_load) loads
 #define KARGS a.nodes, a.recs, a.crecs, a.aux, a.sh, a.view_inv, a.tiles, a.rgba8, a.rgba32f, a.ray_dirs, a.hit_counts, a.stats
-#define GVRT_LAUNCH_SO(L, A, K, P, S, O)                                                                  \
-    do {                                                                                                  \
-        if (a.stats) hipLaunchKernelGGL((k_render<L, A, K, true, P, S, O>), g, b, 0, c->stream, a, KARGS);   \
-        else hipLaunchKernelGGL((k_render<L, A, K, false, P, S, O>), g, b, 0, c->stream, a, KARGS);          \
+    // the kernel-time events ride on the dispatch itself (hipExtLaunchKernelGGL): no separate event packets
+    // between one frame's render and the next launch
+#define GVRT_LAUNCH_SO(L, A, K, P, S, O)                                                                     \
+    do {                                                                                                     \
+        if (a.stats)                                                                                         \
+            hipExtLaunchKernelGGL((k_render<L, A, K, true, P, S, O>), g, b, 0, c->stream, ev_start, ev_stop, 0u, \
+                                  a, KARGS);                                                                 \
+        else                                                                                                 \
+            hipExtLaunchKernelGGL((k_render<L, A, K, false, P, S, O>), g, b, 0, c->stream, ev_start, ev_stop,   \
+                                  0u, a, KARGS);                                                             \
     } while (0)
 #define GVRT_LAUNCH(L, A, K, P) GVRT_LAUNCH_SO(L, A, K, P, true, false)
     // FAST packed kernels also come without the per-child box slack, used when the absolute box padding
