@@ -251,6 +251,7 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
     if (p->collapse > 1) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "collapse must be 0 (greedy) or 1 (SAH-optimal DP)");
     GVRT_HIP(c, hipSetDevice(c->device));
     c->recs_ok = false;
+    c->recs_cams_ok = false;
     gvrt_dfree(c, (void**)&c->d_nodes4x8);
     gvrt_status s = gvrt_launch_build_accel(c, *p);
     if (s) return s;
@@ -669,10 +670,33 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         for (uint32_t i = 1; i < ncams && one_origin; ++i)
             one_origin = std::memcmp(view_inverse + 16ull * i + 12, view_inverse + 12, 12) == 0;
         const bool adaptive = (c->enc.opts & 1u) != 0;
-        a.okrec = c->opt[GVRT_OPT_RECORD_ORIGINS] && one_origin && p->mode == GVRT_MODE_FAST &&
-                  a.kfast == (uint32_t)K_FAST_DEFAULT && !adaptive && a.nrecs < 0xFFFFFFu &&
-                  c->opt[GVRT_OPT_PACKED_KBUFFER] && c->d_leaf_p && !c->split_cells;
-        if (a.okrec) {
+        const bool okbase = c->opt[GVRT_OPT_RECORD_ORIGINS] && p->mode == GVRT_MODE_FAST &&
+                            a.kfast == (uint32_t)K_FAST_DEFAULT && !adaptive && a.nrecs < 0xFFFFFFu &&
+                            c->opt[GVRT_OPT_PACKED_KBUFFER] && c->d_leaf_p && !c->split_cells;
+        a.okrec = okbase && one_origin;
+        const uint64_t cams_bytes = (uint64_t)ncams * c->n_leaves * sizeof(RenderRec);
+        if (okbase && !one_origin && ncams <= 16 && cams_bytes <= (8ull << 30)) {
+            // several origins (a light-field rig): one record copy per camera, written when the set of origins
+            // changes (a static rig: once), and camera c's waves read copy c (RenderArgs::recs_cam_stride)
+            std::vector<float> org(3ull * ncams);
+            for (uint32_t i = 0; i < ncams; ++i)
+                for (int k = 0; k < 3; ++k) org[3ull * i + k] = view_inverse[16ull * i + 12 + k];
+            if (!c->recs_cams_ok || c->recs_cams_origins != org) {
+                if (c->recs_cams_bytes < cams_bytes) {
+                    gvrt_dfree(c, (void**)&c->d_recs_cams);
+                    c->recs_cams_bytes = 0;
+                    if ((s = gvrt_dalloc(c, (void**)&c->d_recs_cams, cams_bytes))) return s;
+                    c->recs_cams_bytes = cams_bytes;
+                }
+                if ((s = gvrt_launch_rec_cams(c, ncams, a.view_inv, c->d_recs_cams))) return s;
+                c->recs_cams_origins = org;
+                c->recs_cams_ok = true;
+            }
+            a.okrec = 1;
+            a.recs = c->d_recs_cams;
+            a.crecs = c->d_recs_cams;
+            a.recs_cam_stride = c->n_leaves;
+        } else if (a.okrec) {
             // the records already hold this origin's kernel-frame origins when the previous launch had the same
             // one (a static camera, or the frames of one view): no pass
             if (!c->recs_ok || std::memcmp(c->rec_origin, view_inverse + 12, 12) != 0) {

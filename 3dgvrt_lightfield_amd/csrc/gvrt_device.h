@@ -103,7 +103,8 @@ struct RenderArgs {
     uint32_t ray_dirs_layout;
     uint32_t packed;
     uint32_t kfast;  // FAST-mode k-buffer depth (8, 12, 16, 24)
-    uint32_t okrec;      // records hold kernel-frame origins for this launch's single camera origin
+    uint32_t okrec;      // records hold kernel-frame origins for this launch's camera origin(s)
+    uint64_t recs_cam_stride;  // okrec with several origins: camera c reads the record copy at recs + c x stride
     const Bvh4Node* nodes8;  // the 4-wide nodes in 8 copies, copy o with each axis a of o's bits stored (hi, lo):
     uint64_t nodes8_stride;  // a wave whose rays share octant o reads (near, far) planes in place (nodes per copy)
     uint32_t box_exact;  // box padding covers the plane rounding for these cameras: no per-child slack

@@ -58,6 +58,12 @@ struct gvrt_context {
     // rec_origin (k_rec_origin), which every other reader must first restore (gvrt_launch_rec_prep op 2)
     bool recs_ok = false;
     float rec_origin[3] = {0, 0, 0};
+    // multi-origin launches (light-field rigs): one record copy per camera with that camera's kernel-frame origins,
+    // kept while the set of origins is unchanged
+    gvrt::RenderRec* d_recs_cams = nullptr;
+    uint64_t recs_cams_bytes = 0;
+    std::vector<float> recs_cams_origins;
+    bool recs_cams_ok = false;
     uint64_t n_leaves = 0;           // BVH leaves: the survivors, or their split pieces
     uint32_t* d_leaf_aux = nullptr;  // split: per leaf {proxy, cell, proxy's cell range lo, hi} (uint4); else null
     uint32_t split_cells = 0;        // grid cells on the longest axis (0: no split)
@@ -152,6 +158,8 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const gvrt::RenderArgs& a, 
 gvrt_status gvrt_launch_tile_order(gvrt_context* c, const uint32_t* codes, int radius);
 // record preparation: op 0 save leaf positions, 1 write kernel-frame origins for o, 2 restore positions
 gvrt_status gvrt_launch_rec_prep(gvrt_context* c, int op, const float* o);
+// multi-origin launches: per-camera record copies (dst = ncams x n_leaves records) for the cameras at d_view_inv
+gvrt_status gvrt_launch_rec_cams(gvrt_context* c, uint32_t ncams, const float* d_view_inv, gvrt::RenderRec* dst);
 // the 8 octant copies of the 4-wide nodes (d_nodes4x8)
 gvrt_status gvrt_launch_node_octants(gvrt_context* c);
 gvrt_status gvrt_launch_unpack(gvrt_context* c, const void* packed, const uint32_t* tiles,

@@ -386,7 +386,7 @@ __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlan
 constexpr uint32_t ST_W = 8, ST_H = 4;
 constexpr int RENDER_MIN_WAVES = 4;
 
-template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK, bool SLACK, bool OKREC>
+template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK, bool SLACK, bool OKREC, bool OKCAM = false>
 __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArgs a, const Bvh4Node* __restrict__ nodes_,
                                                                  const RenderRec* __restrict__ recs_,
                                                                  const RenderRec* __restrict__ crecs_,
@@ -436,6 +436,9 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
         if (tx >= a.tiles_x || ty >= a.tiles_y) return;  // wave-uniform: tile outside the frame
     }
     cam = uni(cam);
+    // OKCAM: a multi-origin launch whose records carry each camera's kernel-frame origins, one copy per camera
+    const RenderRec* __restrict__ recw = OKCAM ? recs_ + (uint64_t)cam * a.recs_cam_stride : recs_;
+    const RenderRec* __restrict__ crecw = OKCAM ? crecs_ + (uint64_t)cam * a.recs_cam_stride : crecs_;
     const uint32_t px = tx * 8 + (lane & 7), py = ty * 8 + (lane >> 3);
     const bool valid = px < a.width && py < a.height && cam < a.ncams;
 
@@ -638,7 +641,7 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                 leafmask &= leafmask - 1;
                 const uint64_t bk = GVRT_PICK(bal, k);
                 const int32_t li = ~GVRT_PICK(ch, k);  // leaf slot
-                const RenderRec rec = load_rec_at(recs_, unii(li));
+                const RenderRec rec = load_rec_at(recw, unii(li));
                 // split (SplitBLAS analogue): the piece's proxy id and cell; cell == ~0u admits every crossing
                 uint4 pa = make_uint4((uint32_t)li, 0xFFFFFFFFu, 0u, 0u);
                 if (aux_) pa = aux_[li];
@@ -764,7 +767,7 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                         }
                         if constexpr (PACK) {
                             // processHit re-evaluates the response of the hit particle (per-lane record load)
-                            const RenderRec rec = crecs_[hid];
+                            const RenderRec rec = crecw[hid];
                             f3 ok, dk;
                             kernel_frame<OKREC>(rec, o, d, ok, dk);
                             const float l2 = len2(dk);
@@ -928,15 +931,16 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
 #define KARGS a.nodes, a.recs, a.crecs, a.aux, a.sh, a.view_inv, a.tiles, a.rgba8, a.rgba32f, a.ray_dirs, a.hit_counts, a.stats
     // the kernel-time events ride on the dispatch itself (hipExtLaunchKernelGGL): no separate event packets
     // between one frame's render and the next launch
-#define GVRT_LAUNCH_SO(L, A, K, P, S, O)                                                                     \
-    do {                                                                                                     \
-        if (a.stats)                                                                                         \
-            hipExtLaunchKernelGGL((k_render<L, A, K, true, P, S, O>), g, b, 0, c->stream, ev_start, ev_stop, 0u, \
-                                  a, KARGS);                                                                 \
-        else                                                                                                 \
-            hipExtLaunchKernelGGL((k_render<L, A, K, false, P, S, O>), g, b, 0, c->stream, ev_start, ev_stop,   \
-                                  0u, a, KARGS);                                                             \
+#define GVRT_LAUNCH_SOC(L, A, K, P, S, O, C)                                                                    \
+    do {                                                                                                        \
+        if (a.stats)                                                                                            \
+            hipExtLaunchKernelGGL((k_render<L, A, K, true, P, S, O, C>), g, b, 0, c->stream, ev_start, ev_stop, 0u, \
+                                  a, KARGS);                                                                    \
+        else                                                                                                    \
+            hipExtLaunchKernelGGL((k_render<L, A, K, false, P, S, O, C>), g, b, 0, c->stream, ev_start, ev_stop,   \
+                                  0u, a, KARGS);                                                                \
     } while (0)
+#define GVRT_LAUNCH_SO(L, A, K, P, S, O) GVRT_LAUNCH_SOC(L, A, K, P, S, O, false)
 #define GVRT_LAUNCH(L, A, K, P) GVRT_LAUNCH_SO(L, A, K, P, true, false)
     // FAST packed kernels also come without the per-child box slack, used when the absolute box padding
     // covers the plane rounding for this launch's cameras (RenderArgs::box_exact, set by render_impl)
@@ -967,7 +971,11 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
             default:
                 // the default depth also reads kernel-frame origins from the records when render_impl
                 // prepared them for a single-origin launch (RenderArgs::okrec)
-                if (a.okrec && a.box_exact) GVRT_LAUNCH_SO(false, false, K_FAST_DEFAULT, true, false, true);
+                // (one record copy per camera for a multi-origin launch: RenderArgs::recs_cam_stride)
+                if (a.okrec && a.recs_cam_stride) {
+                    if (a.box_exact) GVRT_LAUNCH_SOC(false, false, K_FAST_DEFAULT, true, false, true, true);
+                    else GVRT_LAUNCH_SOC(false, false, K_FAST_DEFAULT, true, true, true, true);
+                } else if (a.okrec && a.box_exact) GVRT_LAUNCH_SO(false, false, K_FAST_DEFAULT, true, false, true);
                 else if (a.okrec) GVRT_LAUNCH_SO(false, false, K_FAST_DEFAULT, true, true, true);
                 else GVRT_LAUNCH_F(K_FAST_DEFAULT);
                 break;
@@ -976,6 +984,7 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
 #undef GVRT_LAUNCH
 #undef GVRT_LAUNCH_F
 #undef GVRT_LAUNCH_SO
+#undef GVRT_LAUNCH_SOC
 #undef KARGS
     GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;
@@ -1128,6 +1137,36 @@ __global__ __launch_bounds__(256) void k_rec_origin(uint64_t m, const float* __r
     float4* w = reinterpret_cast<float4*>(recs + i);
     w[0] = make_float4(ok.x, ok.y, ok.z, r.density);
 }
+// Multi-origin launches (a light-field rig): one record copy per camera, copy c holding camera c's origins
+__global__ __launch_bounds__(256) void k_rec_origin_cams(uint64_t m, uint32_t ncams, const float* __restrict__ leaf_p,
+                                                         const RenderRec* __restrict__ src, RenderRec* dst,
+                                                         const float* __restrict__ view_inv) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    RenderRec r = src[i];
+    r.px = leaf_p[3 * i];
+    r.py = leaf_p[3 * i + 1];
+    r.pz = leaf_p[3 * i + 2];
+    for (uint32_t c = 0; c < ncams; ++c) {
+        const float* v = view_inv + 16 * c;
+        const f3 ok = kernel_org(r, mk3(v[12], v[13], v[14]));
+        RenderRec w = r;
+        w.px = ok.x;
+        w.py = ok.y;
+        w.pz = ok.z;
+        dst[(uint64_t)c * m + i] = w;
+    }
+}
+
+gvrt_status gvrt_launch_rec_cams(gvrt_context* c, uint32_t ncams, const float* d_view_inv, RenderRec* dst) {
+    const uint64_t m = c->n_leaves;
+    if (!m || !c->d_leaf_p) return GVRT_OK;
+    hipLaunchKernelGGL(k_rec_origin_cams, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, c->stream, m, ncams,
+                       c->d_leaf_p, c->d_recs, dst, d_view_inv);
+    GVRT_HIP(c, hipGetLastError());
+    return GVRT_OK;
+}
+
 __global__ __launch_bounds__(256) void k_rec_restore(uint64_t m, const float* __restrict__ leaf_p, RenderRec* recs) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;

@@ -589,3 +589,33 @@ def test_read_tile_costs(gv, config1):
         r.render(vi, pi, W, H, tiles=tiles, packed=True)
         cl = r.tile_costs(ntiles=len(tiles))
         assert cl.shape == (len(tiles),) and int(cl.max()) < 64
+
+
+def test_multi_origin_record_copies_change_no_pixel(gv, config1):
+    """A multi-origin FAST launch (a light-field rig) reads one record copy per camera holding that camera's
+    kernel-frame origins (k_rec_origin_cams, RenderArgs::recs_cam_stride): the frames equal those of the
+    record_origins = 0 path (origins recomputed per leaf) bit for bit, for a first rig, the same rig again (copies
+    kept) and a moved rig (copies rewritten), and stay right when a single-origin launch comes in between."""
+    W, H = 96, 64
+    eye = np.array([0.0, 0.3, 3.2])
+    rigs = []
+    for shift in (0.0, 0.4):
+        vis, pi = gv.camera.lightfield_grid_rig(tuple(eye + [shift, 0, 0]), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), nx=2,
+                                                ny=2, spacing=0.15, fovy_deg=45.0, aspect=gv.camera.aspect_ratio(W, H),
+                                                centred=True)
+        rigs.append((np.ascontiguousarray(vis.reshape(-1)), pi))
+    single_vi, single_pi = gv.scene.config1_camera(W, H)
+    outs = {}
+    for ro in (1, 0):
+        with gv.Renderer(0) as r:
+            r.set_option("record_origins", ro)
+            r.prepare(config1)
+            got = [r.render(rigs[0][0], rigs[0][1], W, H, 4)["rgba32f"],
+                   r.render(rigs[0][0], rigs[0][1], W, H, 4)["rgba32f"],
+                   r.render(single_vi, single_pi, W, H)["rgba32f"],
+                   r.render(rigs[1][0], rigs[1][1], W, H, 4)["rgba32f"],
+                   r.render(rigs[0][0], rigs[0][1], W, H, 4)["rgba32f"]]
+        outs[ro] = got
+    for a, b in zip(outs[1], outs[0]):
+        np.testing.assert_array_equal(a, b)
+    assert np.abs(outs[1][0] - outs[1][3]).max() > 0  # the moved rig sees something else
