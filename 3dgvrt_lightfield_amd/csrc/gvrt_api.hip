@@ -250,19 +250,12 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
                          "builder must be 0 (LBVH), 1 (PLOC), 2 (binned SAH, device) or 3 (binned SAH, host)");
     if (p->collapse > 1) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "collapse must be 0 (greedy) or 1 (SAH-optimal DP)");
     GVRT_HIP(c, hipSetDevice(c->device));
-    c->recs_ok = false;
+    c->okrecs_valid[0] = c->okrecs_valid[1] = false;
     c->recs_cams_ok = false;
     gvrt_dfree(c, (void**)&c->d_nodes4x8);
     gvrt_status s = gvrt_launch_build_accel(c, *p);
     if (s) return s;
     if ((s = gvrt_launch_node_octants(c))) return s;
-    // leaf positions, kept aside for the launches whose records carry kernel-frame origins instead
-    gvrt_dfree(c, (void**)&c->d_leaf_p);
-    if (!c->split_cells && c->n_leaves) {
-        if ((s = gvrt_dalloc(c, (void**)&c->d_leaf_p, 12 * c->n_leaves))) return s;
-        if ((s = gvrt_launch_rec_prep(c, 0, nullptr))) return s;
-        GVRT_HIP(c, hipStreamSynchronize(c->stream));
-    }
     return GVRT_OK;
 }
 
@@ -672,7 +665,7 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         const bool adaptive = (c->enc.opts & 1u) != 0;
         const bool okbase = c->opt[GVRT_OPT_RECORD_ORIGINS] && p->mode == GVRT_MODE_FAST &&
                             a.kfast == (uint32_t)K_FAST_DEFAULT && !adaptive && a.nrecs < 0xFFFFFFu &&
-                            c->opt[GVRT_OPT_PACKED_KBUFFER] && c->d_leaf_p && !c->split_cells;
+                            c->opt[GVRT_OPT_PACKED_KBUFFER] && c->n_leaves && !c->split_cells;
         a.okrec = okbase && one_origin;
         const uint64_t cams_bytes = (uint64_t)ncams * c->n_leaves * sizeof(RenderRec);
         if (okbase && !one_origin && ncams <= 16 && cams_bytes <= (8ull << 30)) {
@@ -697,16 +690,35 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
             a.crecs = c->d_recs_cams;
             a.recs_cam_stride = c->n_leaves;
         } else if (a.okrec) {
-            // the records already hold this origin's kernel-frame origins when the previous launch had the same
-            // one (a static camera, or the frames of one view): no pass
-            if (!c->recs_ok || std::memcmp(c->rec_origin, view_inverse + 12, 12) != 0) {
-                if ((s = gvrt_launch_rec_prep(c, 1, view_inverse + 12))) return s;
-                std::memcpy(c->rec_origin, view_inverse + 12, 12);
-                c->recs_ok = true;
+            // a copy already holding this origin's kernel-frame origins (a static camera, the frames of one view,
+            // or a camera coming back): no pass
+            int k = -1;
+            for (int j = 0; j < 2; ++j)
+                if (c->okrecs_valid[j] && c->okrecs_n == c->n_leaves &&
+                    std::memcmp(c->okrecs_origin[j], view_inverse + 12, 12) == 0)
+                    k = j;
+            if (k < 0) {
+                if (c->okrecs_n != c->n_leaves || !c->d_okrecs[0]) {
+                    GVRT_HIP(c, hipStreamSynchronize(c->stream));
+                    for (int j = 0; j < 2; ++j) {
+                        gvrt_dfree(c, (void**)&c->d_okrecs[j]);
+                        c->okrecs_valid[j] = false;
+                    }
+                    c->okrecs_n = 0;
+                    for (int j = 0; j < 2; ++j)
+                        if ((s = gvrt_dalloc(c, (void**)&c->d_okrecs[j], c->n_leaves * sizeof(RenderRec)))) return s;
+                    c->okrecs_n = c->n_leaves;
+                }
+                // the copy not used by the latest launch, rewritten in stream order (after its queued readers);
+                // a side stream overlapping the pass with the previous frame measured slower
+                k = c->okrecs_valid[c->okrecs_cur] ? 1 - c->okrecs_cur : c->okrecs_cur;
+                if ((s = gvrt_launch_rec_origin(c, view_inverse + 12, c->d_okrecs[k], c->stream))) return s;
+                std::memcpy(c->okrecs_origin[k], view_inverse + 12, 12);
+                c->okrecs_valid[k] = true;
             }
-        } else if (c->recs_ok) {
-            if ((s = gvrt_launch_rec_prep(c, 2, nullptr))) return s;
-            c->recs_ok = false;
+            c->okrecs_cur = k;
+            a.recs = c->d_okrecs[k];
+            a.crecs = c->d_okrecs[k];
         }
     }
     if (a.kfast != 8 && a.kfast != 12 && a.kfast != 16 && a.kfast != 20 && a.kfast != 24 && a.kfast != 32)

@@ -53,11 +53,15 @@ struct gvrt_context {
     uint64_t n_nodes4 = 0;
     gvrt::Bvh4Node* d_nodes4x8 = nullptr;  // 8 octant copies of d_nodes4 (planes in near / far order)
     uint32_t* d_leaf_src = nullptr;  // leaf -> compaction index
-    float* d_leaf_p = nullptr;       // leaf positions (3 per leaf): d_recs keeps ok in their place while recs_ok
-    // d_recs positions are valid only while !recs_ok: while recs_ok they hold the kernel-frame origins of
-    // rec_origin (k_rec_origin), which every other reader must first restore (gvrt_launch_rec_prep op 2)
-    bool recs_ok = false;
-    float rec_origin[3] = {0, 0, 0};
+    // Single-origin FAST launches read one of two copies of the leaf records whose positions are replaced by the
+    // launch camera's kernel-frame origin (k_rec_origin, in stream order); d_recs itself always keeps the
+    // positions, so no other reader has to restore anything.  Two copies: a camera that comes back to the
+    // previous origin (alternating views) finds its copy still written.
+    gvrt::RenderRec* d_okrecs[2] = {nullptr, nullptr};
+    uint64_t okrecs_n = 0;
+    float okrecs_origin[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    bool okrecs_valid[2] = {false, false};
+    int okrecs_cur = 0;
     // multi-origin launches (light-field rigs): one record copy per camera with that camera's kernel-frame origins,
     // kept while the set of origins is unchanged
     gvrt::RenderRec* d_recs_cams = nullptr;
@@ -157,7 +161,8 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const gvrt::RenderArgs& a, 
 // codes: the tile list the order is over (cam << 24 | ty << 12 | tx); radius > 0: classes spread by a max filter
 gvrt_status gvrt_launch_tile_order(gvrt_context* c, const uint32_t* codes, int radius);
 // record preparation: op 0 save leaf positions, 1 write kernel-frame origins for o, 2 restore positions
-gvrt_status gvrt_launch_rec_prep(gvrt_context* c, int op, const float* o);
+// k_rec_origin: dst = d_recs with each position replaced by the kernel-frame origin of o, on `stream`
+gvrt_status gvrt_launch_rec_origin(gvrt_context* c, const float* o, gvrt::RenderRec* dst, hipStream_t stream);
 // multi-origin launches: per-camera record copies (dst = ncams x n_leaves records) for the cameras at d_view_inv
 gvrt_status gvrt_launch_rec_cams(gvrt_context* c, uint32_t ncams, const float* d_view_inv, gvrt::RenderRec* dst);
 // the 8 octant copies of the 4-wide nodes (d_nodes4x8)

@@ -1122,31 +1122,27 @@ gvrt_status gvrt_launch_tile_order(gvrt_context* c, const uint32_t* codes, int r
     return GVRT_OK;
 }
 
-// Per-launch record preparation for single-origin FAST launches: each leaf record's position is replaced by
-// its kernel-frame origin ok = S^-1 R^T (o - p) (kernel_org, the arithmetic the render kernel would do per
-// leaf visit and per composited hit); k_rec_restore puts the positions back for launches that need them.
-__global__ __launch_bounds__(256) void k_rec_origin(uint64_t m, const float* __restrict__ leaf_p, RenderRec* recs,
+// Record copies for FAST launches: each leaf record with its position replaced by its kernel-frame origin
+// ok = S^-1 R^T (o - p) of the launch camera (kernel_org, the arithmetic the render kernel would otherwise do per
+// leaf visit and per composited hit).  d_recs keeps the positions.
+__global__ __launch_bounds__(256) void k_rec_origin(uint64_t m, const RenderRec* __restrict__ src, RenderRec* dst,
                                                     float ox, float oy, float oz) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
-    RenderRec r = recs[i];
-    r.px = leaf_p[3 * i];
-    r.py = leaf_p[3 * i + 1];
-    r.pz = leaf_p[3 * i + 2];
+    RenderRec r = src[i];
     const f3 ok = kernel_org(r, mk3(ox, oy, oz));
-    float4* w = reinterpret_cast<float4*>(recs + i);
-    w[0] = make_float4(ok.x, ok.y, ok.z, r.density);
+    r.px = ok.x;
+    r.py = ok.y;
+    r.pz = ok.z;
+    dst[i] = r;
 }
+
 // Multi-origin launches (a light-field rig): one record copy per camera, copy c holding camera c's origins
-__global__ __launch_bounds__(256) void k_rec_origin_cams(uint64_t m, uint32_t ncams, const float* __restrict__ leaf_p,
-                                                         const RenderRec* __restrict__ src, RenderRec* dst,
-                                                         const float* __restrict__ view_inv) {
+__global__ __launch_bounds__(256) void k_rec_origin_cams(uint64_t m, uint32_t ncams, const RenderRec* __restrict__ src,
+                                                         RenderRec* dst, const float* __restrict__ view_inv) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
-    RenderRec r = src[i];
-    r.px = leaf_p[3 * i];
-    r.py = leaf_p[3 * i + 1];
-    r.pz = leaf_p[3 * i + 2];
+    const RenderRec r = src[i];
     for (uint32_t c = 0; c < ncams; ++c) {
         const float* v = view_inv + 16 * c;
         const f3 ok = kernel_org(r, mk3(v[12], v[13], v[14]));
@@ -1160,35 +1156,18 @@ __global__ __launch_bounds__(256) void k_rec_origin_cams(uint64_t m, uint32_t nc
 
 gvrt_status gvrt_launch_rec_cams(gvrt_context* c, uint32_t ncams, const float* d_view_inv, RenderRec* dst) {
     const uint64_t m = c->n_leaves;
-    if (!m || !c->d_leaf_p) return GVRT_OK;
+    if (!m) return GVRT_OK;
     hipLaunchKernelGGL(k_rec_origin_cams, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, c->stream, m, ncams,
-                       c->d_leaf_p, c->d_recs, dst, d_view_inv);
+                       c->d_recs, dst, d_view_inv);
     GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;
 }
 
-__global__ __launch_bounds__(256) void k_rec_restore(uint64_t m, const float* __restrict__ leaf_p, RenderRec* recs) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    recs[i].px = leaf_p[3 * i];
-    recs[i].py = leaf_p[3 * i + 1];
-    recs[i].pz = leaf_p[3 * i + 2];
-}
-__global__ __launch_bounds__(256) void k_rec_save(uint64_t m, const RenderRec* __restrict__ recs, float* leaf_p) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    leaf_p[3 * i] = recs[i].px;
-    leaf_p[3 * i + 1] = recs[i].py;
-    leaf_p[3 * i + 2] = recs[i].pz;
-}
-
-gvrt_status gvrt_launch_rec_prep(gvrt_context* c, int op, const float* o) {
+gvrt_status gvrt_launch_rec_origin(gvrt_context* c, const float* o, RenderRec* dst, hipStream_t stream) {
     const uint64_t m = c->n_leaves;
-    if (!m || !c->d_leaf_p) return GVRT_OK;
-    const dim3 g((unsigned)((m + 255) / 256)), b(256);
-    if (op == 0) hipLaunchKernelGGL(k_rec_save, g, b, 0, c->stream, m, c->d_recs, c->d_leaf_p);
-    else if (op == 1) hipLaunchKernelGGL(k_rec_origin, g, b, 0, c->stream, m, c->d_leaf_p, c->d_recs, o[0], o[1], o[2]);
-    else hipLaunchKernelGGL(k_rec_restore, g, b, 0, c->stream, m, c->d_leaf_p, c->d_recs);
+    if (!m) return GVRT_OK;
+    hipLaunchKernelGGL(k_rec_origin, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, m, c->d_recs, dst,
+                       o[0], o[1], o[2]);
     GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;
 }

@@ -619,3 +619,30 @@ def test_multi_origin_record_copies_change_no_pixel(gv, config1):
     for a, b in zip(outs[1], outs[0]):
         np.testing.assert_array_equal(a, b)
     assert np.abs(outs[1][0] - outs[1][3]).max() > 0  # the moved rig sees something else
+
+
+def test_origin_record_copies_queued_moving_camera(gv, config1):
+    """Single-origin FAST launches read one of two origin record copies; a new camera origin is written, in
+    stream order, into the copy the latest launch did not use.  Eight frames queued back to back
+    (gvrt_render_async) with origins A B A C D D A E — new origins, returns to a kept copy, repeats — each equal
+    bit for bit the synchronous frame of the record_origins = 0 path (origins recomputed per leaf)."""
+    import torch
+    W, H = 128, 96
+    eyes = {"A": (0.0, 0.3, 3.2), "B": (0.5, 0.2, 3.0), "C": (-0.4, 0.5, 3.3), "D": (0.2, -0.3, 3.1),
+            "E": (0.9, 0.4, 2.8)}
+    seq = "ABACDDAE"
+    cams = {k: gv.camera.pinhole(e, (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 40.0, W / H) for k, e in eyes.items()}
+    with gv.Renderer(0) as r:
+        r.set_option("record_origins", 0)
+        r.prepare(config1)
+        ref = {k: r.render(vi, pi, W, H, rgba8=False)["rgba32f"] for k, (vi, pi) in cams.items()}
+    dev = torch.device("cuda", 0)
+    bufs = [torch.zeros((H, W, 4), dtype=torch.float32, device=dev) for _ in seq]
+    with gv.Renderer(0) as r:
+        r.prepare(config1)
+        for k, b in zip(seq, bufs):
+            vi, pi = cams[k]
+            r.render_device(vi, pi, W, H, rgba32f_ptr=b.data_ptr(), async_=True)
+        r.sync()
+    for k, b in zip(seq, bufs):
+        np.testing.assert_array_equal(b.cpu().numpy().reshape(ref[k].shape), ref[k])
