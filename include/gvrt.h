@@ -252,8 +252,9 @@ gvrt_status gvrt_get_device_buffers(gvrt_handle h, gvrt_device_buffers* out);
                                        per-tile costs; 0: supertile order */
 #define GVRT_OPT_TILE_XCD 1u        /* 1 (default): each cost class dealt to the 8 XCDs in contiguous chunks */
 #define GVRT_OPT_OCTANT_NODES 2u    /* 1 (default): waves read the octant copy of the nodes (8x node memory) */
-#define GVRT_OPT_RECORD_ORIGINS 3u  /* 1 (default): single-origin FAST launches read kernel-frame origins
-                                       written into the leaf records by one pass per camera origin */
+#define GVRT_OPT_RECORD_ORIGINS 3u  /* 1 (default): FAST launches read copies of the leaf records holding each
+                                       camera's kernel-frame origins, written by one pass per camera origin (kept
+                                       while the origins stay the same; up to 16 cameras per launch) */
 #define GVRT_OPT_BOX_SLACK 4u       /* 0 (default): per-child exit slack only when the box padding does not
                                        cover the plane rounding for the launch's cameras; 1: always */
 #define GVRT_OPT_PACKED_KBUFFER 5u  /* 1 (default): packed FAST k-buffer when record ids fit 24 bits; 0: the
