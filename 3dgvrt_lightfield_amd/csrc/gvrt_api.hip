@@ -253,6 +253,9 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
     c->okrecs_valid[0] = c->okrecs_valid[1] = false;
     c->recs_cams_ok = false;
     gvrt_dfree(c, (void**)&c->d_nodes4x8);
+    gvrt_dfree(c, (void**)&c->d_nodes4e);
+    gvrt_dfree(c, (void**)&c->d_nodes4ex8);
+    c->accept_ok = false;
     gvrt_status s = gvrt_launch_build_accel(c, *p);
     if (s) return s;
     if ((s = gvrt_launch_node_octants(c))) return s;
@@ -655,6 +658,18 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
                       std::ldexp(omax, -20) <= c->box_pad_abs;  // also false for a NaN origin
     }
     a.kfast = p->kbuffer_depth ? p->kbuffer_depth : (uint32_t)K_FAST_DEFAULT;
+    // FAST launches traverse the acceptance-box nodes (gvrt_launch_accept_nodes), refit when the acceptance
+    // thresholds change; LITERAL launches keep every crossing and so the proxy boxes
+    if (p->mode == GVRT_MODE_FAST && c->opt[GVRT_OPT_ACCEPT_BOXES] && !c->split_cells &&
+        (p->hit_min_gaussian_response > 0.0f || p->alpha_min > 0.0f) && a.nrecs < 0xFFFFFFu &&
+        c->opt[GVRT_OPT_PACKED_KBUFFER]) {
+        if (!c->accept_ok || c->accept_key[0] != p->hit_min_gaussian_response || c->accept_key[1] != p->alpha_min)
+            if ((s = gvrt_launch_accept_nodes(c, p->hit_min_gaussian_response, p->alpha_min))) return s;
+        if (c->accept_ok) {
+            a.nodes = c->d_nodes4e;
+            a.nodes8 = c->opt[GVRT_OPT_OCTANT_NODES] ? c->d_nodes4ex8 : nullptr;
+        }
+    }
     // Single-origin FAST launches at the default depth read each leaf's kernel-frame origin ok from its record:
     // one pass per launch writes ok = S^-1 R^T (o - p) in place of the position (k_rec_origin), instead of
     // every leaf visit and composited hit of every wave recomputing it.  Other launches get the positions back.

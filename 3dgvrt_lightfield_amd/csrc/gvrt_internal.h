@@ -53,6 +53,12 @@ struct gvrt_context {
     uint64_t n_nodes4 = 0;
     gvrt::Bvh4Node* d_nodes4x8 = nullptr;  // 8 octant copies of d_nodes4 (planes in near / far order)
     uint32_t* d_leaf_src = nullptr;  // leaf -> compaction index
+    // FAST launches: the 4-wide nodes with acceptance boxes (gvrt_launch_accept_nodes), plain and in 8 octant
+    // copies, for the acceptance thresholds in accept_key (refit when a launch brings other thresholds)
+    gvrt::Bvh4Node* d_nodes4e = nullptr;
+    gvrt::Bvh4Node* d_nodes4ex8 = nullptr;
+    float accept_key[2] = {0.0f, 0.0f};
+    bool accept_ok = false;
     // Single-origin FAST launches read one of two copies of the leaf records whose positions are replaced by the
     // launch camera's kernel-frame origin (k_rec_origin, in stream order); d_recs itself always keeps the
     // positions, so no other reader has to restore anything.  Two copies: a camera that comes back to the
@@ -131,7 +137,7 @@ struct gvrt_context {
 
     gvrt_stats stats{};
     // per-handle tuning switches (gvrt_set_option), measured-best defaults
-    int64_t opt[GVRT_OPT_COUNT] = {1, 1, 1, 1, 0, 1, 0};
+    int64_t opt[GVRT_OPT_COUNT] = {1, 1, 1, 1, 0, 1, 0, 1};
 };
 
 gvrt_status gvrt_fail(gvrt_context* c, gvrt_status code, const std::string& msg);
@@ -167,5 +173,7 @@ gvrt_status gvrt_launch_rec_origin(gvrt_context* c, const float* o, gvrt::Render
 gvrt_status gvrt_launch_rec_cams(gvrt_context* c, uint32_t ncams, const float* d_view_inv, gvrt::RenderRec* dst);
 // the 8 octant copies of the 4-wide nodes (d_nodes4x8)
 gvrt_status gvrt_launch_node_octants(gvrt_context* c);
+// FAST launches: d_nodes4e (+ octant copies d_nodes4ex8) with acceptance boxes for these thresholds
+gvrt_status gvrt_launch_accept_nodes(gvrt_context* c, float min_response, float alpha_min);
 gvrt_status gvrt_launch_unpack(gvrt_context* c, const void* packed, const uint32_t* tiles,
                                uint64_t ntiles, uint32_t width, uint32_t height, void* frame);

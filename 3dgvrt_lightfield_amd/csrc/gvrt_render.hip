@@ -582,7 +582,16 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                 t_node0 = __builtin_amdgcn_s_memtime();  // the node phase includes the fetch
             }
             const NodeS nd = load_node_at(nbase, unii(cur));  // whole node: 2x s_load_dwordx16
-            const float tc = fminf(fminf(thi, kt[KB - 1]), tcut);
+            float tc = fminf(fminf(thi, kt[KB - 1]), tcut);
+            float tl = tlo;
+            if constexpr (PACK) {
+                // acceptance-box nodes (FAST): the leaf children's boxes bound each particle's acceptance ellipsoid,
+                // which lies within the node's D (pad[2]) of an admitted crossing along the ray, so the range is
+                // widened by D; nodes with inner children and the proxy-box nodes carry D = 0
+                const float dn = __int_as_float(unii(NODE_PAD(nd, 2)));
+                tl = tlo - dn;
+                tc = tc + dn;
+            }
             uint64_t bal[BVH_W];
             if (octw) {
                 // (an opaque copy of 1/d: otherwise the first child's plane FMAs, common to both tests, are hoisted
@@ -593,13 +602,13 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                 for (int k = 0; k < BVH_W; ++k)
                     bal[k] = __builtin_amdgcn_ballot_w64(
                         box_hit_nf<SLACK>(NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 1),
-                                          NODE_BOX(nd, k, 3), NODE_BOX(nd, k, 5), oinv, iv, tlo, tc));
+                                          NODE_BOX(nd, k, 3), NODE_BOX(nd, k, 5), oinv, iv, tl, tc));
             } else {
 #pragma unroll
                 for (int k = 0; k < BVH_W; ++k)  // compare results straight to SGPR masks
                     bal[k] = __builtin_amdgcn_ballot_w64(
                         box_hit<SLACK>(NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 1),
-                                       NODE_BOX(nd, k, 3), NODE_BOX(nd, k, 5), oinv, inv, tlo, tc));
+                                       NODE_BOX(nd, k, 3), NODE_BOX(nd, k, 5), oinv, inv, tl, tc));
             }
             int32_t ch[BVH_W];
 #pragma unroll
@@ -1205,6 +1214,110 @@ gvrt_status gvrt_launch_node_octants(gvrt_context* c) {
     hipLaunchKernelGGL(k_node_octants, dim3((unsigned)((8 * n + 255) / 256)), dim3(256), 0, c->stream, n, c->d_nodes4,
                        c->d_nodes4x8);
     GVRT_HIP(c, hipGetLastError());
+    return GVRT_OK;
+}
+
+// ---- Acceptance boxes (FAST launches, handle option GVRT_OPT_ACCEPT_BOXES).
+// In FAST mode only accepted crossings enter the k-buffer, and a crossing of particle P is accepted only if
+// gres > hitMinGaussianResponse and min(0.99, gres * density) > alphaMinThreshold (gaussianfunctions.glsl:192-200),
+// i.e. gres > m = max(min_response, alpha_min / density), with gres = exp(S d^4) and d the distance of the ray's
+// line from P's centre in the kernel frame.  So the line passes through the ball E = {|x_k| <= r}, r^4 = ln(m) / S.
+// The proxy's AABB is larger (the icosahedron's circumradius is Rc = 1.258 kS, r <= kS when min_response is the
+// enclosing pass's kernel response, and r shrinks with density).  In this copy of the nodes the leaves of every
+// all-leaf node get the boxes of E, and particles that can never be accepted (density <= alpha_min) are dropped
+// everywhere.  The admitted crossing (entry or exit face, in (tlo, tc]) lies on the proxy and, along the line, at
+// most sqrt(Rc^2 - r^2) (kernel frame) from E's chord, i.e. D = s_max sqrt(Rc^2 - r^2) in t, so an all-leaf node's
+// children are tested over [tlo - D, tc + D], D the largest of its leaves' (pad[2]; 0 elsewhere and in the
+// proxy-box nodes).  Nodes with inner children keep their proxy boxes: one D per node would widen the inner
+// children's range too (every node on E boxes refit upwards, or a per-child D, measured slower: DESIGN.md §4).
+// Which crossings are admitted does not change, only which leaves a wave visits.
+constexpr float ICO_CIRCUM = 1.2584086f;  // icosahedron circumradius / inradius
+__device__ inline bool slot_empty(const Bvh4Node& n, int k) { return n.box[k][0] > 1e37f; }
+__device__ inline void set_empty(Bvh4Node& n, int k) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j) n.box[k][j] = EMPTY_BOX;
+}
+
+struct AcceptArgs {
+    float min_response, alpha_min, kmin, kdeg, pad_abs;
+    uint32_t kopts;
+};
+
+__global__ __launch_bounds__(256) void k_accept_leaf(uint64_t n, const Bvh4Node* __restrict__ src,
+                                                     const RenderRec* __restrict__ recs, AcceptArgs p,
+                                                     Bvh4Node* __restrict__ dst) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Bvh4Node nd = src[i];
+    float dmax = 0.0f;
+    // a node with inner children keeps its leaves' proxy boxes (D = 0 would not cover the acceptance boxes, and a
+    // D > 0 would widen the inner children's range too); only never-accepted leaves are dropped there
+    const bool all_leaves = nd.pad[1] == 0u;
+#pragma unroll
+    for (int k = 0; k < BVH_W; ++k) {
+        if (slot_empty(nd, k) || nd.child[k] >= 0) continue;
+        const RenderRec r = recs[~nd.child[k]];
+        const float rho = r.density;
+        // (alpha_min >= 0.99: galpha = min(0.99, .) never exceeds it)
+        const float m = fmaxf(p.min_response, p.alpha_min / rho);  // > 0 (render_impl: min_response or alpha_min > 0)
+        if (!(rho > p.alpha_min) || !(m < 1.0f) || !(p.alpha_min < 0.99f)) {
+            set_empty(nd, k);
+            continue;
+        }
+        if (!all_leaves) continue;
+        const float re = powf(logf(m) / KERNEL_S, 0.25f) * 1.01f;  // 1 % margin on r
+        const float sx = 1.0f / r.isx, sy = 1.0f / r.isy, sz = 1.0f / r.isz;
+        // world = p + R diag(s) x_k; row i of R diag(s) = (c_i.x sx, c_i.y sy, c_i.z sz) (kernel_org's columns)
+        const float hx = re * sqrtf(r.c0x * r.c0x * sx * sx + r.c0y * r.c0y * sy * sy + r.c0z * r.c0z * sz * sz);
+        const float hy = re * sqrtf(r.c1x * r.c1x * sx * sx + r.c1y * r.c1y * sy * sy + r.c1z * r.c1z * sz * sz);
+        const float hz = re * sqrtf(r.c2x * r.c2x * sx * sx + r.c2y * r.c2y * sy * sy + r.c2z * r.c2z * sz * sz);
+        const float c3[3] = {r.px, r.py, r.pz}, h3[3] = {hx, hy, hz};
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) {
+            // the proxy boxes' padding (gvrt_enclose.hip), so the render kernel's plane rounding is covered alike
+            const float lo = c3[ax] - h3[ax] * 1.0001f, hi = c3[ax] + h3[ax] * 1.0001f;
+            const float pad = 1e-5f * (hi - lo) + 1e-6f * fabsf(c3[ax]) + p.pad_abs + 1e-30f;
+            nd.box[k][2 * ax] = lo - pad;
+            nd.box[k][2 * ax + 1] = hi + pad;
+        }
+        // the icosahedron the render kernel clips against: inradius kS (kernel_scale with the enclosing options)
+        const float rc = ICO_CIRCUM * 1.001f * kernel_scale(rho, p.kmin, p.kopts, p.kdeg);
+        const float gap = sqrtf(fmaxf(rc * rc - re * re, 0.0f));
+        dmax = fmaxf(dmax, gap * fmaxf(sx, fmaxf(sy, sz)) * 1.01f + 4.0f * p.pad_abs);
+    }
+    nd.pad[2] = __float_as_uint(dmax);
+    dst[i] = nd;
+}
+
+gvrt_status gvrt_launch_accept_nodes(gvrt_context* c, float min_response, float alpha_min) {
+    const uint64_t n = c->n_nodes4;
+    c->accept_ok = false;
+    if (!n || !c->d_nodes4 || c->split_cells) return GVRT_OK;
+    gvrt_status s;
+    if (!c->d_nodes4e) {
+        if ((s = gvrt_dalloc(c, (void**)&c->d_nodes4e, n * sizeof(Bvh4Node)))) return s;
+        // octant copies: without them (no memory) the octant waves read the plain acceptance nodes
+        if (gvrt_dalloc(c, (void**)&c->d_nodes4ex8, 8 * n * sizeof(Bvh4Node)) != GVRT_OK) {
+            c->d_nodes4ex8 = nullptr;
+            c->err.clear();
+        }
+    }
+    AcceptArgs p;
+    p.min_response = min_response;
+    p.alpha_min = alpha_min;
+    p.kmin = c->enc.kernel_min_response;
+    p.kdeg = c->enc.degree;
+    p.kopts = c->enc.opts;
+    p.pad_abs = c->box_pad_abs;
+    hipLaunchKernelGGL(k_accept_leaf, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, n, c->d_nodes4,
+                       c->d_recs, p, c->d_nodes4e);
+    if (c->d_nodes4ex8)
+        hipLaunchKernelGGL(k_node_octants, dim3((unsigned)((8 * n + 255) / 256)), dim3(256), 0, c->stream, n,
+                           c->d_nodes4e, c->d_nodes4ex8);
+    GVRT_HIP(c, hipGetLastError());
+    c->accept_key[0] = min_response;
+    c->accept_key[1] = alpha_min;
+    c->accept_ok = true;
     return GVRT_OK;
 }
 

@@ -262,7 +262,11 @@ gvrt_status gvrt_get_device_buffers(gvrt_handle h, gvrt_device_buffers* out);
 #define GVRT_OPT_ORDER_SPREAD 6u    /* 0..8 (default 0): the least radius, in tiles, by which the previous launch's
                                        tile costs are spread (max filter) before ordering; the camera's motion sets
                                        it otherwise (0 for a static camera) */
-#define GVRT_OPT_COUNT 7u
+#define GVRT_OPT_ACCEPT_BOXES 7u   /* 1 (default): FAST launches traverse a copy of the 4-wide nodes in which the
+                                       leaves of all-leaf nodes have the boxes of their acceptance ellipsoids (for
+                                       the launch's hit_min_gaussian_response / alpha_min) and particles that can
+                                       never be accepted are dropped; 0: the proxy boxes */
+#define GVRT_OPT_COUNT 8u
 gvrt_status gvrt_set_option(gvrt_handle h, uint32_t option, int64_t value);
 gvrt_status gvrt_get_option(gvrt_handle h, uint32_t option, int64_t* value);
 

@@ -539,7 +539,7 @@ def test_unpacked_fast_path_matches(gv, config1):
     np.testing.assert_allclose(outs[0], outs[1], rtol=0, atol=1e-6)
 
 
-@pytest.mark.parametrize("option", ["tile_order", "tile_xcd", "octant_nodes", "record_origins", "box_slack",
+@pytest.mark.parametrize("option", ["tile_order", "tile_xcd", "octant_nodes", "record_origins", "box_slack", "accept_boxes",
                                     "order_spread"])
 def test_tuning_options_change_no_pixel(gv, config1, option):
     """Each per-handle tuning switch (gvrt_set_option) changes how the frame is computed, never a pixel:
@@ -558,6 +558,27 @@ def test_tuning_options_change_no_pixel(gv, config1, option):
             r.set_option(option, 9 if option == "order_spread" else 2)
     for a, b in zip(ref, got):
         np.testing.assert_array_equal(a, b)
+
+
+def test_accept_boxes_follow_the_thresholds(gv):
+    """The acceptance-box nodes (option accept_boxes) are refit whenever a launch brings other acceptance thresholds
+    (hit_min_gaussian_response, alpha_min), including thresholds that drop most particles (alpha_min 0.2: faint
+    particles are never accepted) and a min_response below the enclosing kernel response (acceptance ellipsoid
+    larger than the proxy's inscribed sphere): every frame equals the frame with the option off, bit for bit.
+    Dense stand-in subset (opacity logit N(-3, 2): most particles faint)."""
+    s = gv.scene.dense_standin(60_000, seed=4)
+    W, H = 192, 128
+    vi, pi = gv.scene.mipnerf_camera(W, H)
+    cases = [{}, dict(alpha_min=0.2), dict(hit_min_gaussian_response=0.004), {}, dict(alpha_min=0.02)]
+    frames = {}
+    for opt in (1, 0):
+        with gv.Renderer(0) as r:
+            r.set_option("accept_boxes", opt)
+            r.prepare(s, builder=2, collapse=1)
+            frames[opt] = [r.render(vi, pi, W, H, **kw)["rgba32f"] for kw in cases for _ in range(2)]
+    for a, b in zip(frames[1], frames[0]):
+        np.testing.assert_array_equal(a, b)
+    assert not np.array_equal(frames[1][0], frames[1][2])  # the thresholds do change the image
 
 
 def test_read_tile_costs(gv, config1):
