@@ -1258,6 +1258,8 @@ __global__ __launch_bounds__(256) void k_accept_leaf(uint64_t n, const Bvh4Node*
         if (slot_empty(nd, k) || nd.child[k] >= 0) continue;
         const RenderRec r = recs[~nd.child[k]];
         const float rho = r.density;
+        // a NaN density keeps its proxy box: the render's min(0.99, gres * NaN) is 0.99, i.e. accepted
+        if (rho != rho) continue;
         // (alpha_min >= 0.99: galpha = min(0.99, .) never exceeds it)
         const float m = fmaxf(p.min_response, p.alpha_min / rho);  // > 0 (render_impl: min_response or alpha_min > 0)
         if (!(rho > p.alpha_min) || !(m < 1.0f) || !(p.alpha_min < 0.99f)) {

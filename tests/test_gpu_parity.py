@@ -565,8 +565,9 @@ def test_accept_boxes_follow_the_thresholds(gv):
     (hit_min_gaussian_response, alpha_min), including thresholds that drop most particles (alpha_min 0.2: faint
     particles are never accepted) and a min_response below the enclosing kernel response (acceptance ellipsoid
     larger than the proxy's inscribed sphere): every frame equals the frame with the option off, bit for bit.
-    Dense stand-in subset (opacity logit N(-3, 2): most particles faint)."""
+    Dense stand-in subset (opacity logit N(-3, 2): most particles faint), with a few NaN opacities."""
     s = gv.scene.dense_standin(60_000, seed=4)
+    s["opacity"][:40] = np.nan  # NaN density: the render accepts it (min(0.99, gres * NaN) = 0.99), so it keeps its box
     W, H = 192, 128
     vi, pi = gv.scene.mipnerf_camera(W, H)
     cases = [{}, dict(alpha_min=0.2), dict(hit_min_gaussian_response=0.004), {}, dict(alpha_min=0.02)]
