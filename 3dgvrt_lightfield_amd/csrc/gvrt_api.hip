@@ -256,6 +256,7 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
     gvrt_dfree(c, (void**)&c->d_nodes4e);
     gvrt_dfree(c, (void**)&c->d_nodes4ex8);
     c->accept_ok = false;
+    c->accept_nomem = false;
     gvrt_status s = gvrt_launch_build_accel(c, *p);
     if (s) return s;
     if ((s = gvrt_launch_node_octants(c))) return s;

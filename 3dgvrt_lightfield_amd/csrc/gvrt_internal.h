@@ -59,6 +59,7 @@ struct gvrt_context {
     gvrt::Bvh4Node* d_nodes4ex8 = nullptr;
     float accept_key[2] = {0.0f, 0.0f};
     bool accept_ok = false;
+    bool accept_nomem = false;  // the acceptance copy did not fit (until the next build)
     // Single-origin FAST launches read one of two copies of the leaf records whose positions are replaced by the
     // launch camera's kernel-frame origin (k_rec_origin, in stream order); d_recs itself always keeps the
     // positions, so no other reader has to restore anything.  Two copies: a camera that comes back to the

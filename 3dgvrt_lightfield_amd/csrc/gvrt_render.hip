@@ -1295,9 +1295,15 @@ gvrt_status gvrt_launch_accept_nodes(gvrt_context* c, float min_response, float 
     const uint64_t n = c->n_nodes4;
     c->accept_ok = false;
     if (!n || !c->d_nodes4 || c->split_cells) return GVRT_OK;
-    gvrt_status s;
     if (!c->d_nodes4e) {
-        if ((s = gvrt_dalloc(c, (void**)&c->d_nodes4e, n * sizeof(Bvh4Node)))) return s;
+        // without the memory FAST launches keep the proxy-box nodes (no retry until the next build)
+        if (c->accept_nomem) return GVRT_OK;
+        if (gvrt_dalloc(c, (void**)&c->d_nodes4e, n * sizeof(Bvh4Node)) != GVRT_OK) {
+            c->d_nodes4e = nullptr;
+            c->err.clear();
+            c->accept_nomem = true;
+            return GVRT_OK;
+        }
         // octant copies: without them (no memory) the octant waves read the plain acceptance nodes
         if (gvrt_dalloc(c, (void**)&c->d_nodes4ex8, 8 * n * sizeof(Bvh4Node)) != GVRT_OK) {
             c->d_nodes4ex8 = nullptr;
