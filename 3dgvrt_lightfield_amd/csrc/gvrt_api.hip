@@ -43,6 +43,18 @@ gvrt_status gvrt_dalloc(gvrt_context* c, void** p, uint64_t bytes) {
     return GVRT_OK;
 }
 
+bool gvrt_dalloc_optional(gvrt_context* c, void** p, uint64_t bytes) {
+    *p = nullptr;
+    const int64_t cap_mb = c->opt[GVRT_OPT_OPTIONAL_MEM_MB];
+    if (cap_mb > 0 && c->device_bytes + bytes > ((uint64_t)cap_mb << 20)) return false;
+    if (gvrt_dalloc(c, p, bytes) != GVRT_OK) {
+        *p = nullptr;
+        c->err.clear();
+        return false;
+    }
+    return true;
+}
+
 void gvrt_dfree(gvrt_context* c, void** p) {
     if (!*p) return;
     auto it = c->allocs.find(*p);
@@ -252,6 +264,7 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
     GVRT_HIP(c, hipSetDevice(c->device));
     c->okrecs_valid[0] = c->okrecs_valid[1] = false;
     c->recs_cams_ok = false;
+    c->okrecs_nomem = c->recs_cams_nomem = false;
     gvrt_dfree(c, (void**)&c->d_nodes4x8);
     gvrt_dfree(c, (void**)&c->d_nodes4e);
     gvrt_dfree(c, (void**)&c->d_nodes4ex8);
@@ -327,10 +340,12 @@ gvrt_status gvrt_get_device_buffers(gvrt_handle c, gvrt_device_buffers* out) {
 gvrt_status gvrt_set_option(gvrt_handle c, uint32_t option, int64_t value) {
     if (!c) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL handle");
     if (option >= GVRT_OPT_COUNT) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "unknown option");
-    const int64_t vmax = option == GVRT_OPT_ORDER_SPREAD ? 8 : 1;
+    const int64_t vmax = option == GVRT_OPT_ORDER_SPREAD ? 8 : (option == GVRT_OPT_OPTIONAL_MEM_MB ? (1ll << 40) : 1);
     if (value < 0 || value > vmax)
-        return gvrt_fail(c, GVRT_ERR_INVALID_ARG, option == GVRT_OPT_ORDER_SPREAD ? "order spread is 0..8 tiles"
-                                                                                  : "option values are 0 or 1");
+        return gvrt_fail(c, GVRT_ERR_INVALID_ARG,
+                         option == GVRT_OPT_ORDER_SPREAD       ? "order spread is 0..8 tiles"
+                         : option == GVRT_OPT_OPTIONAL_MEM_MB ? "optional memory limit is 0..2^40 MiB"
+                                                              : "option values are 0 or 1");
     if (c->opt[option] == value) return GVRT_OK;
     GVRT_HIP(c, hipSetDevice(c->device));
     if (c->async_pending) GVRT_HIP(c, hipStreamSynchronize(c->stream));  // queued launches used the old value
@@ -684,23 +699,52 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
                             c->opt[GVRT_OPT_PACKED_KBUFFER] && c->n_leaves && !c->split_cells;
         a.okrec = okbase && one_origin;
         const uint64_t cams_bytes = (uint64_t)ncams * c->n_leaves * sizeof(RenderRec);
-        if (okbase && !one_origin && ncams <= 16 && cams_bytes <= (8ull << 30)) {
+        // (the copies are an optional speed-up: one that does not fit leaves the launch on d_recs, okrec = 0, until
+        // the next build)
+        bool cams_ready = false;
+        if (okbase && !one_origin && ncams <= 16 && cams_bytes <= (8ull << 30) && !c->recs_cams_nomem) {
             // several origins (a light-field rig): one record copy per camera, written when the set of origins
             // changes (a static rig: once), and camera c's waves read copy c (RenderArgs::recs_cam_stride)
             std::vector<float> org(3ull * ncams);
             for (uint32_t i = 0; i < ncams; ++i)
                 for (int k = 0; k < 3; ++k) org[3ull * i + k] = view_inverse[16ull * i + 12 + k];
-            if (!c->recs_cams_ok || c->recs_cams_origins != org) {
+            cams_ready = c->recs_cams_ok && c->recs_cams_origins == org;
+            if (!cams_ready) {
                 if (c->recs_cams_bytes < cams_bytes) {
+                    if (c->d_recs_cams) GVRT_HIP(c, hipStreamSynchronize(c->stream));  // queued launches read it
                     gvrt_dfree(c, (void**)&c->d_recs_cams);
                     c->recs_cams_bytes = 0;
-                    if ((s = gvrt_dalloc(c, (void**)&c->d_recs_cams, cams_bytes))) return s;
-                    c->recs_cams_bytes = cams_bytes;
+                    c->recs_cams_ok = false;
+                    if (gvrt_dalloc_optional(c, (void**)&c->d_recs_cams, cams_bytes)) c->recs_cams_bytes = cams_bytes;
+                    else c->recs_cams_nomem = true;
                 }
-                if ((s = gvrt_launch_rec_cams(c, ncams, a.view_inv, c->d_recs_cams))) return s;
-                c->recs_cams_origins = org;
-                c->recs_cams_ok = true;
+                if (!c->recs_cams_nomem) {
+                    if ((s = gvrt_launch_rec_cams(c, ncams, a.view_inv, c->d_recs_cams))) return s;
+                    c->recs_cams_origins = org;
+                    c->recs_cams_ok = true;
+                    cams_ready = true;
+                }
             }
+        }
+        if (a.okrec && !c->okrecs_nomem && (c->okrecs_n != c->n_leaves || !c->d_okrecs[0])) {
+            GVRT_HIP(c, hipStreamSynchronize(c->stream));
+            for (int j = 0; j < 2; ++j) {
+                gvrt_dfree(c, (void**)&c->d_okrecs[j]);
+                c->okrecs_valid[j] = false;
+            }
+            c->okrecs_n = 0;
+            bool ok = true;
+            for (int j = 0; j < 2 && ok; ++j)
+                ok = gvrt_dalloc_optional(c, (void**)&c->d_okrecs[j], c->n_leaves * sizeof(RenderRec));
+            if (ok) {
+                c->okrecs_n = c->n_leaves;
+            } else {
+                for (int j = 0; j < 2; ++j) gvrt_dfree(c, (void**)&c->d_okrecs[j]);
+                c->okrecs_nomem = true;
+            }
+        }
+        if (c->okrecs_nomem) a.okrec = 0;
+        if (cams_ready) {
             a.okrec = 1;
             a.recs = c->d_recs_cams;
             a.crecs = c->d_recs_cams;
@@ -714,17 +758,6 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
                     std::memcmp(c->okrecs_origin[j], view_inverse + 12, 12) == 0)
                     k = j;
             if (k < 0) {
-                if (c->okrecs_n != c->n_leaves || !c->d_okrecs[0]) {
-                    GVRT_HIP(c, hipStreamSynchronize(c->stream));
-                    for (int j = 0; j < 2; ++j) {
-                        gvrt_dfree(c, (void**)&c->d_okrecs[j]);
-                        c->okrecs_valid[j] = false;
-                    }
-                    c->okrecs_n = 0;
-                    for (int j = 0; j < 2; ++j)
-                        if ((s = gvrt_dalloc(c, (void**)&c->d_okrecs[j], c->n_leaves * sizeof(RenderRec)))) return s;
-                    c->okrecs_n = c->n_leaves;
-                }
                 // the copy not used by the latest launch, rewritten in stream order (after its queued readers);
                 // a side stream overlapping the pass with the previous frame measured slower
                 k = c->okrecs_valid[c->okrecs_cur] ? 1 - c->okrecs_cur : c->okrecs_cur;

@@ -69,12 +69,14 @@ struct gvrt_context {
     float okrecs_origin[2][3] = {{0, 0, 0}, {0, 0, 0}};
     bool okrecs_valid[2] = {false, false};
     int okrecs_cur = 0;
+    bool okrecs_nomem = false;  // the copies did not fit (until the next build): launches read d_recs
     // multi-origin launches (light-field rigs): one record copy per camera with that camera's kernel-frame origins,
     // kept while the set of origins is unchanged
     gvrt::RenderRec* d_recs_cams = nullptr;
     uint64_t recs_cams_bytes = 0;
     std::vector<float> recs_cams_origins;
     bool recs_cams_ok = false;
+    bool recs_cams_nomem = false;  // the per-camera copies did not fit (until the next build)
     uint64_t n_leaves = 0;           // BVH leaves: the survivors, or their split pieces
     uint32_t* d_leaf_aux = nullptr;  // split: per leaf {proxy, cell, proxy's cell range lo, hi} (uint4); else null
     uint32_t split_cells = 0;        // grid cells on the longest axis (0: no split)
@@ -138,13 +140,17 @@ struct gvrt_context {
 
     gvrt_stats stats{};
     // per-handle tuning switches (gvrt_set_option), measured-best defaults
-    int64_t opt[GVRT_OPT_COUNT] = {1, 1, 1, 1, 0, 1, 0, 1};
+    int64_t opt[GVRT_OPT_COUNT] = {1, 1, 1, 1, 0, 1, 0, 1, 0};
 };
 
 gvrt_status gvrt_fail(gvrt_context* c, gvrt_status code, const std::string& msg);
 gvrt_status gvrt_hip_check(gvrt_context* c, hipError_t e, const char* what);
 gvrt_status gvrt_dalloc(gvrt_context* c, void** p, uint64_t bytes);
 void gvrt_dfree(gvrt_context* c, void** p);
+// An optional speed-up copy (octant nodes, acceptance nodes, record-origin copies): false, with no error left on the
+// handle, when it does not fit (hipMalloc fails, or the handle's device bytes would exceed GVRT_OPT_OPTIONAL_MEM_MB);
+// the caller then runs without the copy
+bool gvrt_dalloc_optional(gvrt_context* c, void** p, uint64_t bytes);
 
 #define GVRT_HIP(ctx, expr)                                         \
     do {                                                            \

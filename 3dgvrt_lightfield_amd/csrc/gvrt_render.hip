@@ -1,7 +1,7 @@
 // gvrt_render.hip — Particle Rendering pass on gfx950.
 //
 // Replaces the per-pixel ray-march of shaders/glsl/VulkanFullRT/particleRendering.comp:117-191
-// (ray query), raygen.rgen:303-383 + anyhit.rahit:40-71 (RT pipeline) and
+// (ray query), raygen.rgen:113-193 + anyhit.rahit:40-71 (RT pipeline) and
 // raygenGaussianLightField.rgen:114-202 (multi-camera light field), and the driver's BVH
 // traversal behind traceRayEXT / rayQueryProceedEXT.
 //
@@ -1206,11 +1206,7 @@ gvrt_status gvrt_launch_node_octants(gvrt_context* c) {
     const uint64_t n = c->n_nodes4;
     if (!n || !c->d_nodes4) return GVRT_OK;
     // 8 x the node array (0.46 GB at 1 M Gaussians); when it does not fit, waves read the plain nodes
-    if (gvrt_dalloc(c, (void**)&c->d_nodes4x8, 8 * n * sizeof(Bvh4Node)) != GVRT_OK) {
-        c->d_nodes4x8 = nullptr;
-        c->err.clear();
-        return GVRT_OK;
-    }
+    if (!gvrt_dalloc_optional(c, (void**)&c->d_nodes4x8, 8 * n * sizeof(Bvh4Node))) return GVRT_OK;
     hipLaunchKernelGGL(k_node_octants, dim3((unsigned)((8 * n + 255) / 256)), dim3(256), 0, c->stream, n, c->d_nodes4,
                        c->d_nodes4x8);
     GVRT_HIP(c, hipGetLastError());
@@ -1266,7 +1262,9 @@ __global__ __launch_bounds__(256) void k_accept_leaf(uint64_t n, const Bvh4Node*
             set_empty(nd, k);
             continue;
         }
-        if (!all_leaves) continue;
+        // (a non-positive density with a negative alpha_min is accepted outside a shell, not inside a ball:
+        // sigmoid-activated densities are positive, but such a leaf keeps its proxy box)
+        if (!all_leaves || !(rho > 0.0f)) continue;
         const float re = powf(logf(m) / KERNEL_S, 0.25f) * 1.01f;  // 1 % margin on r
         const float sx = 1.0f / r.isx, sy = 1.0f / r.isy, sz = 1.0f / r.isz;
         // world = p + R diag(s) x_k; row i of R diag(s) = (c_i.x sx, c_i.y sy, c_i.z sz) (kernel_org's columns)
@@ -1298,17 +1296,12 @@ gvrt_status gvrt_launch_accept_nodes(gvrt_context* c, float min_response, float 
     if (!c->d_nodes4e) {
         // without the memory FAST launches keep the proxy-box nodes (no retry until the next build)
         if (c->accept_nomem) return GVRT_OK;
-        if (gvrt_dalloc(c, (void**)&c->d_nodes4e, n * sizeof(Bvh4Node)) != GVRT_OK) {
-            c->d_nodes4e = nullptr;
-            c->err.clear();
+        if (!gvrt_dalloc_optional(c, (void**)&c->d_nodes4e, n * sizeof(Bvh4Node))) {
             c->accept_nomem = true;
             return GVRT_OK;
         }
         // octant copies: without them (no memory) the octant waves read the plain acceptance nodes
-        if (gvrt_dalloc(c, (void**)&c->d_nodes4ex8, 8 * n * sizeof(Bvh4Node)) != GVRT_OK) {
-            c->d_nodes4ex8 = nullptr;
-            c->err.clear();
-        }
+        (void)gvrt_dalloc_optional(c, (void**)&c->d_nodes4ex8, 8 * n * sizeof(Bvh4Node));
     }
     AcceptArgs p;
     p.min_response = min_response;

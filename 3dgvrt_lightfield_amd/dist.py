@@ -1,11 +1,15 @@
 """Multi-GPU frame split + exchange: one process per GPU, scene and BVH replicated per
 rank, one exchange per frame.
 
-  * tile split  (strong scaling, config 4): 64x64-pixel blocks (8x8 of the kernel's 8x8 tiles)
-    round-robin over ranks; each rank renders its tiles tile-packed, the parts are gathered to rank 0
-    with torch.distributed (backend 'nccl' = RCCL over xGMI on MI355X, 'gloo' on CPU for tests) and
-    scattered into the frame (gvrt_unpack_tiles_rgba8 on the GPU, unpack_tiles_host on the CPU).
-  * view split  (weak scaling, light-field config 5): whole views round-robin over ranks.
+  * tile split  (strong scaling, config 4): by default contiguous bands of the frame's 64x64-pixel blocks
+    (8x8 of the kernel's 8x8 tiles), cut where the summed per-tile cost of a calibration frame reaches
+    k/N of the total (band_tiles over cost_weights; bench.py --tile-layout cost-bands), or 64x64-pixel
+    blocks round-robin over ranks (rank_tiles, --tile-layout blocks); each rank renders its tiles
+    tile-packed, the parts go to rank 0 with exact-size point-to-point sends (torch.distributed, backend
+    'nccl' = RCCL over xGMI on MI355X, 'gloo' on CPU for tests) and are scattered into the frame
+    (gvrt_unpack_tiles_rgba8 on the GPU, unpack_tiles_host on the CPU).
+  * view split  (light-field config 5, and one view per rank for the weak-scaling line): whole views,
+    cost-balanced (balanced_views) when there are more views than ranks, else round-robin (rank_views).
 
 `FrameExchange` is the double-buffered exchange bench.py runs; the renderer and the rank-0 assembly are
 injected, so the same object is driven by the gloo tests on CPU (tests/test_dist.py).  `launch_ranks`
@@ -104,18 +108,22 @@ def unpack_tiles_host(packed, tiles, width, height, ncams=1, frame=None):
 class FrameExchange:
     """Double-buffered frame exchange, the one exchange step per frame of SURVEY §8e.
 
-    Every rank owns `nbuf` send buffers of one padded part shape (collective gathers need equal shapes:
-    the largest rank's part).  step(render) waits until the gather that last used buffer b has completed
-    (and lets rank 0 assemble that frame), renders the next frame into buffer b, and posts its gather to
-    rank 0 asynchronously, so the gather of frame i (RCCL on torch's stream) overlaps the render of frame
-    i + 1 (the library's HIP stream).  drain() completes every outstanding frame.
+    Every rank owns `nbuf` send buffers of exactly its own part size; rank 0 owns `nbuf` receive buffers per other
+    rank, each exactly that rank's part size.  The exchange is point to point (batch_isend_irecv: every rank r > 0
+    sends its part to rank 0, rank 0 receives each; rank 0's own part never leaves its send buffer), so unequal
+    parts move no padding (round 3 gathered every part padded to the largest one: up to 28 % extra bytes with cost
+    bands).  step(render) waits until the exchange that last used buffer b has completed (and lets rank 0 assemble
+    that frame), renders the next frame into buffer b, and posts its sends / receives asynchronously, so the
+    exchange of frame i (RCCL on its own stream) overlaps the render of frame i + 1 (the library's HIP stream).
+    drain() completes every outstanding frame.
 
-      render(buf)             writes this rank's part of the next frame into `buf` (a view of the send
-                              buffer of this rank's own part size)
-      assemble(parts, frame)  rank 0 only: builds the frame from the gathered parts (list of world tensors,
-                              each cut to its rank's part size); frame counts from 0
-      sync()                  called after a gather completed and before its buffers are reused or read
-                              by another stream (torch.cuda.current_stream().synchronize on the GPU)
+      render(buf)             writes this rank's part of the next frame into `buf` (its send buffer)
+      assemble(parts, frame)  rank 0 only: builds the frame from the parts (list of world tensors, rank r's of its
+                              part size); frame counts from 0
+      sync()                  called after an exchange completed and before its buffers are reused or read by
+                              another stream (torch.cuda.current_stream().synchronize on the GPU)
+      mark(name)              optional, probe() only: called at "rendered" (render posted), "exchanged" (the
+                              exchange waited for) and "assembled"; the bench records HIP events there
     """
 
     def __init__(self, dist, rank, world, part_sizes, item_shape, dtype, device="cpu", nbuf=2, assemble=None,
@@ -124,10 +132,11 @@ class FrameExchange:
 
         self.dist, self.rank, self.world = dist, rank, world
         self.part_sizes = [int(s) for s in part_sizes]
-        maxn = max(self.part_sizes)
-        shape = (maxn,) + tuple(item_shape)
-        self.send = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(nbuf)]
-        self.recv = [[torch.empty(shape, dtype=dtype, device=device) for _ in range(world)] if rank == 0 else None
+        self.item_shape = tuple(item_shape)
+        self.send = [torch.zeros((self.part_sizes[rank],) + self.item_shape, dtype=dtype, device=device)
+                     for _ in range(nbuf)]
+        self.recv = [[None if r == 0 else torch.empty((self.part_sizes[r],) + self.item_shape, dtype=dtype,
+                                                      device=device) for r in range(world)] if rank == 0 else None
                      for _ in range(nbuf)]
         self.pending = [None] * nbuf
         self.frame_of = [None] * nbuf
@@ -135,23 +144,39 @@ class FrameExchange:
         self.assemble = assemble
         self.sync = sync
         self.frames = 0
+        item_bytes = int(np.prod(self.item_shape, dtype=np.int64)) * torch.empty((), dtype=dtype).element_size()
+        # what crosses the links per frame (rank r > 0's part to rank 0), and what a padded gather moved instead
+        self.exchange_bytes = sum(self.part_sizes[1:]) * item_bytes
+        self.padded_gather_bytes = (world - 1) * max(self.part_sizes) * item_bytes
+
+    def parts(self, b):
+        """Rank 0: every rank's part of the frame in buffer b (rank 0's own part is its send buffer)."""
+        return [self.send[b]] + list(self.recv[b][1:])
+
+    def _post(self, b):
+        d = self.dist
+        if self.rank == 0:
+            ops = [d.P2POp(d.irecv, self.recv[b][r], r) for r in range(1, self.world) if self.part_sizes[r]]
+        else:
+            ops = [d.P2POp(d.isend, self.send[b], 0)] if self.part_sizes[self.rank] else []
+        return d.batch_isend_irecv(ops) if ops else []
 
     def _finish(self, b):
         if self.pending[b] is None:
             return
-        self.pending[b].wait()
+        for w in self.pending[b]:
+            w.wait()
         if self.sync:
             self.sync()
         if self.rank == 0 and self.assemble:
-            self.assemble([p[:n] for p, n in zip(self.recv[b], self.part_sizes)], self.frame_of[b])
+            self.assemble(self.parts(b), self.frame_of[b])
         self.pending[b] = None
 
     def step(self, render):
         b = self.frames % self.nbuf
         self._finish(b)
-        render(self.send[b][: self.part_sizes[self.rank]])
-        self.pending[b] = self.dist.gather(self.send[b], self.recv[b] if self.rank == 0 else None, dst=0,
-                                           async_op=True)
+        render(self.send[b])
+        self.pending[b] = self._post(b)
         self.frame_of[b] = self.frames
         self.frames += 1
 
@@ -159,12 +184,34 @@ class FrameExchange:
         for k in range(self.nbuf):
             self._finish((self.frames + k) % self.nbuf)
 
+    def probe(self, render, mark, barrier=None):
+        """One frame with nothing else in flight, for the per-phase times of the strong-scaling record: render,
+        (barrier: every rank has rendered), exchange, wait, assemble, with mark() at each boundary ("rendered",
+        "posted", "exchanged", "assembled").  Call after drain()."""
+        self.drain()
+        b = self.frames % self.nbuf
+        render(self.send[b])
+        mark("rendered")
+        if barrier:
+            barrier()
+        mark("posted")
+        w = self._post(b)
+        for x in w:
+            x.wait()
+        mark("exchanged")
+        if self.sync:
+            self.sync()
+        if self.rank == 0 and self.assemble:
+            self.assemble(self.parts(b), self.frames)
+        mark("assembled")
+        self.frames += 1
+
 
 def gather_tiles(dist, part, rank, world, sizes, device=None):
     """Gather tile-packed parts (uint8 [n_r*64, 4] tensors) to rank 0 (one synchronous exchange)."""
     ex = FrameExchange(dist, rank, world, sizes, part.shape[1:], part.dtype, part.device, nbuf=1)
     out = []
-    ex.assemble = lambda parts, _f: out.extend(parts)
+    ex.assemble = lambda parts, _f: out.extend(p.clone() for p in parts)
     ex.step(lambda buf: buf.copy_(part))
     ex.drain()
     return out if rank == 0 else None

@@ -14,6 +14,10 @@
 //                        prints one JSON line)
 //   gvrt_app cameras    [--width W --height H] [--transforms T]   (prints the camera matrices; no GPU)
 //   gvrt_app png        OUT.png                                   (writes a test pattern; no GPU)
+//   gvrt_app split      ... --layout views [--views V] (config 5: the views of a V-camera light-field rig split
+//                       over the ranks by cost, each view gathered whole to rank 0; checked against one batched
+//                       render of the whole rig on rank 0's GPU)
+//   gvrt_app views      --costs c0,c1,... --world N (the cost-balanced view assignment, one rank per line; no GPU)
 //   gvrt_app tiles      --rank R --world N [--width W --height H] [--layout blocks|bands --costs F]
 //                       (this rank's split tile list; F: raw uint8 cost classes [ty][tx]; no GPU)
 #include <cmath>
@@ -84,10 +88,11 @@ gm::vec3 parse_vec3(const std::string& s) {
 
 int usage() {
     std::fprintf(stderr,
-                 "usage: gvrt_app {render|eval|lightfield|hitcounts|bench|split|cameras|png} [--ply P] [--out D]\n"
+                 "usage: gvrt_app {render|eval|lightfield|hitcounts|bench|split|views|tiles|cameras|png} [--ply P] [--out D]\n"
                  "       [--width W] [--height H] [--camera orbit|config1] [--variant rq|rt] [--transforms T]\n"
                  "       [--duration S] [--warmup S] [--frametimes] [--split-cells N] [--build fast|quality]\n"
-                 "       [--device I] [--rank R --world N --id-file F --frames K]\n");
+                 "       [--device I] [--rank R --world N --id-file F --frames K --layout cost-bands|blocks|views --views V]\n"
+                 "       [--costs c0,c1,... (views)]\n");
     return 2;
 }
 
@@ -130,6 +135,23 @@ int main(int argc, char** argv) {
                 tl = gvrt_host::rank_tiles(W, H, 1, rank, world);
             }
             for (const gvrt_tile& t : tl) std::printf("%u %u %u\n", t.tx, t.ty, t.cam);
+            return 0;
+        }
+        if (a.cmd == "views") {  // host-only: the cost-balanced view split (balanced_views), one rank per line
+            std::vector<double> costs;
+            std::string c = a.get("costs");
+            for (size_t p = 0; p < c.size();) {
+                size_t q = c.find(',', p);
+                if (q == std::string::npos) q = c.size();
+                costs.push_back(std::strtod(c.substr(p, q - p).c_str(), nullptr));
+                p = q + 1;
+            }
+            const int world = std::atoi(a.get("world", "1").c_str());
+            if (world < 1) throw std::runtime_error("--world must be >= 1");
+            for (const auto& g : gvrt_host::balanced_views(costs, world)) {
+                for (size_t i = 0; i < g.size(); ++i) std::printf(i ? " %u" : "%u", g[i]);
+                std::printf("\n");
+            }
             return 0;
         }
         if (a.cmd == "cameras") {  // host-only: the camera matrices the C-ABI receives (uint32 bit patterns)
@@ -207,19 +229,39 @@ int main(int argc, char** argv) {
         } else if (a.cmd == "split") {
             const int rank = std::atoi(a.get("rank", "0").c_str()), world = std::atoi(a.get("world", "1").c_str());
             const int frames = std::atoi(a.get("frames", "10").c_str());
+            const std::string lay = a.get("layout", "cost-bands");
+            const bool by_views = lay == "views";
             ncclUniqueId id;
             std::string err;
             if (gvrt_host::rccl_rendezvous(a.get("id-file", out + "/rccl.id"), rank, &id, &err) != GVRT_OK)
                 throw std::runtime_error(err);
             app.updateUniformBuffer(cam);
+            // --layout views: config 5, the views of a light-field rig (calculateGaussianLightFieldSamples with
+            // --views cameras, the light-field raygen's pixel centres and alpha start) split over the ranks
+            std::vector<gm::mat4> rig;
+            gm::mat4 rig_pi{};
+            uint32_t nv = 1;
+            if (by_views) {
+                nv = (uint32_t)std::atoi(a.get("views", "16").c_str());
+                gvrt_host::lightfield_ring_rig(app.gModel.splatSet, nv, W, H, rig, rig_pi);
+                app.params.pixel_offset = 0.5f;
+                app.params.alpha_init = 1.0f;
+            }
+            if (a.has("tile-order-off")) {  // fault injection: no cost-ordered launch, so no tile costs to read
+                if (gvrt_set_option(app.handle(), GVRT_OPT_TILE_ORDER, 0) != GVRT_OK) throw std::runtime_error("option");
+            }
+            const size_t frame_bytes = (size_t)4 * W * H * nv;
             void* frame = nullptr;
-            if (rank == 0 && hipMalloc(&frame, (size_t)4 * W * H) != hipSuccess) throw std::runtime_error("frame alloc");
-            std::vector<uint8_t> got((size_t)4 * W * H), one((size_t)4 * W * H);
+            if (rank == 0 && hipMalloc(&frame, frame_bytes) != hipSuccess) throw std::runtime_error("frame alloc");
+            std::vector<uint8_t> got(frame_bytes), one(frame_bytes);
             double ms = 0.0;
+            std::string assignment;
             {
-                const auto layout = a.get("layout", "cost-bands") == "blocks" ? gvrt_host::SplitFrame::BLOCKS
-                                                                              : gvrt_host::SplitFrame::COST_BANDS;
-                gvrt_host::SplitFrame sf(app, rank, world, id, W, H, layout);
+                const auto layout = by_views ? gvrt_host::SplitFrame::VIEWS
+                                    : lay == "blocks" ? gvrt_host::SplitFrame::BLOCKS
+                                                      : gvrt_host::SplitFrame::COST_BANDS;
+                gvrt_host::SplitFrame sf(app, rank, world, id, W, H, layout, by_views ? &rig : nullptr,
+                                         by_views ? &rig_pi : nullptr);
                 if (sf.status() != GVRT_OK) throw std::runtime_error("SplitFrame: " + sf.error());
                 if (sf.draw(frame) != GVRT_OK || sf.sync() != GVRT_OK) throw std::runtime_error(sf.error());  // warm-up
                 const auto t0 = std::chrono::steady_clock::now();
@@ -229,14 +271,30 @@ int main(int argc, char** argv) {
                 ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / frames;
                 if (rank == 0 && hipMemcpy(got.data(), frame, got.size(), hipMemcpyDeviceToHost) != hipSuccess)
                     throw std::runtime_error("frame readback");
+                for (size_t r = 0; r < sf.views().size(); ++r) {
+                    assignment += r ? ", [" : "[";
+                    for (size_t i = 0; i < sf.views()[r].size(); ++i)
+                        assignment += (i ? ", " : "") + std::to_string(sf.views()[r][i]);
+                    assignment += "]";
+                }
             }
             if (rank == 0) {
                 (void)hipFree(frame);
-                app.draw(cam, W, H, one.data());  // the same frame on this GPU alone
+                if (by_views) {  // the whole rig in one batched launch on this GPU alone
+                    std::vector<float> vis;
+                    for (const gm::mat4& m : rig) vis.insert(vis.end(), m.data(), m.data() + 16);
+                    gvrt_image img{one.data(), nullptr, nullptr, nullptr, 0, 0};
+                    if (gvrt_render(app.handle(), &app.params, vis.data(), rig_pi.data(), W, H, nv, nullptr, 0, &img) !=
+                        GVRT_OK)
+                        throw std::runtime_error(std::string("gvrt_render: ") + gvrt_last_error(app.handle()));
+                } else {
+                    app.draw(cam, W, H, one.data());  // the same frame on this GPU alone
+                }
                 const bool same = got == one;
                 if (!write_png(out + "/split_frame.png", got.data(), W, H)) throw std::runtime_error("cannot write png");
-                std::printf("{\"world\": %d, \"frames\": %d, \"ms_per_frame\": %.4f, \"identical_to_one_gpu\": %s}\n",
-                            world, frames, ms, same ? "true" : "false");
+                std::printf("{\"world\": %d, \"frames\": %d, \"views\": %u, \"ms_per_frame\": %.4f, "
+                            "\"identical_to_one_gpu\": %s, \"assignment\": [%s]}\n",
+                            world, frames, nv, ms, same ? "true" : "false", assignment.c_str());
                 if (!same) return 3;
             }
         } else if (a.cmd == "bench") {  // vks::Benchmark (seconds are whole, as benchmark.hpp's uint32_t)

@@ -60,6 +60,29 @@ std::vector<std::vector<gvrt_tile>> band_tiles(uint32_t width, uint32_t height, 
     return out;
 }
 
+std::vector<std::vector<uint32_t>> balanced_views(const std::vector<double>& costs, int world) {
+    // dist.balanced_views: longest-processing-time list scheduling with a count bound
+    const size_t n = costs.size();
+    std::vector<size_t> cap(world);
+    for (int r = 0; r < world; ++r) cap[r] = n / world + ((size_t)r < n % world ? 1 : 0);
+    std::vector<double> load(world, 0.0);
+    std::vector<std::vector<uint32_t>> out(world);
+    std::vector<uint32_t> order(n);
+    for (size_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        return costs[a] > costs[b] || (costs[a] == costs[b] && a < b);  // sorted by (-cost, index)
+    });
+    for (uint32_t v : order) {
+        int best = -1;
+        for (int r = 0; r < world; ++r)
+            if (out[r].size() < cap[r] && (best < 0 || load[r] < load[best])) best = r;  // ties: lower rank
+        out[best].push_back(v);
+        load[best] += costs[v];
+    }
+    for (auto& g : out) std::sort(g.begin(), g.end());
+    return out;
+}
+
 gvrt_status rccl_rendezvous(const std::string& path, int rank, ncclUniqueId* id, std::string* err, double timeout_s) {
     if (rank == 0) {
         const ncclResult_t r = ncclGetUniqueId(id);
@@ -108,42 +131,161 @@ gvrt_status SplitFrame::rccl(ncclResult_t r, const char* what) {
     return fail(GVRT_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
+gvrt_status SplitFrame::agree(gvrt_status local) {
+    // every rank enters this all-reduce (max of the status magnitudes) before anything rank-specific, so a set-up
+    // failure on one rank is every rank's failure and nobody waits in a later collective
+    int32_t* d = nullptr;
+    if (hipMalloc(&d, sizeof(int32_t)) != hipSuccess) {
+        abort_comm();  // cannot take part: the peers' all-reduce errors out
+        return fail(GVRT_ERR_OOM, "status word");
+    }
+    const int32_t mine = -(int32_t)local;  // statuses are <= 0
+    gvrt_status s = GVRT_OK;
+    if (hipMemcpy(d, &mine, sizeof(mine), hipMemcpyHostToDevice) != hipSuccess) s = fail(GVRT_ERR_HIP, "status upload");
+    // (a failed upload still enters the all-reduce: the word then holds garbage, which can only look worse)
+    if (rccl(ncclAllReduce(d, d, 1, ncclInt32, ncclMax, comm_, stream_), "ncclAllReduce")) {
+        (void)hipFree(d);
+        return st_;
+    }
+    int32_t all = 0;
+    if (hipStreamSynchronize(stream_) != hipSuccess || hipMemcpy(&all, d, sizeof(all), hipMemcpyDeviceToHost) != hipSuccess)
+        s = fail(GVRT_ERR_HIP, "status readback");
+    (void)hipFree(d);
+    if (s == GVRT_OK && all != 0) s = fail((gvrt_status)(-all), local != GVRT_OK ? err_ : "set-up failed on another rank");
+    return s == GVRT_OK ? GVRT_OK : st_;
+}
+
+void SplitFrame::abort_comm() {
+    if (comm_) {
+        (void)ncclCommAbort(comm_);
+        comm_ = nullptr;
+    }
+}
+
 gvrt_status SplitFrame::cost_classes(std::vector<uint8_t>* classes) {
     gvrt_handle h = app_.handle();
     const uint64_t n = (uint64_t)((width_ + 7) / 8) * ((height_ + 7) / 8);
     classes->assign(n, 0);
+    // broadcast payload: one status byte (0: rank 0 measured the classes) then the classes
     uint8_t* d = nullptr;
-    if (hipMalloc(&d, std::max<uint64_t>(n, (uint64_t)4 * width_ * height_)) != hipSuccess)
-        return fail(GVRT_ERR_OOM, "cost-class buffer");
-    gvrt_status s = GVRT_OK;
+    gvrt_status local = GVRT_OK;
+    if (hipMalloc(&d, std::max<uint64_t>(n + 1, (uint64_t)4 * width_ * height_)) != hipSuccess) {
+        d = nullptr;
+        local = fail(GVRT_ERR_OOM, "cost-class buffer");
+    }
+    if (agree(local) != GVRT_OK) {
+        if (d) (void)hipFree(d);
+        return st_;
+    }
+    std::string why;
     if (rank_ == 0) {
         // the full frame twice: the second launch is cost-ordered and records every tile's class again
         gvrt_image img{d, nullptr, nullptr, nullptr, 1, 0};
-        for (int k = 0; k < 2 && s == GVRT_OK; ++k)
-            if (gvrt_render_async(h, &app_.params, app_.uniformDataDynamic.viewInverse.data(),
-                                  app_.uniformDataDynamic.projInverse.data(), width_, height_, 1, nullptr, 0,
-                                  &img) != GVRT_OK ||
-                gvrt_sync(h) != GVRT_OK)
-                s = fail(GVRT_ERR_HIP, std::string("calibration render: ") + gvrt_last_error(h));
-        if (s == GVRT_OK && gvrt_read_tile_costs(h, classes->data(), n) != GVRT_OK)
-            s = fail(GVRT_ERR_HIP, std::string("gvrt_read_tile_costs: ") + gvrt_last_error(h));
-        if (s == GVRT_OK && hipMemcpy(d, classes->data(), n, hipMemcpyHostToDevice) != hipSuccess)
-            s = fail(GVRT_ERR_HIP, "class upload");
+        bool ok = true;
+        for (int k = 0; k < 2 && ok; ++k)
+            ok = gvrt_render_async(h, &app_.params, app_.uniformDataDynamic.viewInverse.data(),
+                                   app_.uniformDataDynamic.projInverse.data(), width_, height_, 1, nullptr, 0,
+                                   &img) == GVRT_OK &&
+                 gvrt_sync(h) == GVRT_OK;
+        if (!ok) why = std::string("calibration render: ") + gvrt_last_error(h);
+        if (ok && gvrt_read_tile_costs(h, classes->data(), n) != GVRT_OK) {
+            ok = false;
+            why = std::string("gvrt_read_tile_costs: ") + gvrt_last_error(h);
+        }
+        std::vector<uint8_t> msg(n + 1, 0);
+        msg[0] = ok ? 0 : 1;
+        if (ok) std::copy(classes->begin(), classes->end(), msg.begin() + 1);
+        if (hipMemcpy(d, msg.data(), n + 1, hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipMemset(d, 1, 1);  // best effort: the peers learn of the failure from the status byte
+            if (ok) why = "class upload";
+        }
     }
-    // one broadcast at set-up (not per frame): every rank cuts the same bands from the same classes
-    if (s == GVRT_OK) s = rccl(ncclBroadcast(d, d, n, ncclUint8, 0, comm_, stream_), "ncclBroadcast");
-    if (s == GVRT_OK && hipStreamSynchronize(stream_) != hipSuccess) s = fail(GVRT_ERR_HIP, "broadcast sync");
-    if (s == GVRT_OK && hipMemcpy(classes->data(), d, n, hipMemcpyDeviceToHost) != hipSuccess)
+    // one broadcast at set-up (not per frame), entered by every rank whatever rank 0's calibration gave: every rank
+    // cuts the same bands from the same classes, or learns that there are none
+    if (rccl(ncclBroadcast(d, d, n + 1, ncclUint8, 0, comm_, stream_), "ncclBroadcast")) {
+        (void)hipFree(d);
+        return st_;
+    }
+    std::vector<uint8_t> msg(n + 1, 1);
+    gvrt_status s = GVRT_OK;
+    if (hipStreamSynchronize(stream_) != hipSuccess) s = fail(GVRT_ERR_HIP, "broadcast sync");
+    if (s == GVRT_OK && hipMemcpy(msg.data(), d, n + 1, hipMemcpyDeviceToHost) != hipSuccess)
         s = fail(GVRT_ERR_HIP, "class readback");
     (void)hipFree(d);
+    if (s == GVRT_OK && msg[0] != 0)
+        s = fail(GVRT_ERR_STATE, "tile-cost calibration failed on rank 0" + (why.empty() ? std::string() : ": " + why));
+    if (s == GVRT_OK) std::copy(msg.begin() + 1, msg.end(), classes->begin());
+    return s;
+}
+
+gvrt_status SplitFrame::view_costs_bcast(std::vector<double>* costs) {
+    gvrt_handle h = app_.handle();
+    const size_t nv = rig_.size();
+    costs->assign(nv, 0.0);
+    // broadcast payload: a status word (0.0: rank 0 timed every view) then one kernel time per view
+    double* d = nullptr;
+    void* img_buf = nullptr;
+    gvrt_status local = GVRT_OK;
+    if (hipMalloc(&d, sizeof(double) * (nv + 1)) != hipSuccess) {
+        d = nullptr;
+        local = fail(GVRT_ERR_OOM, "view-cost buffer");
+    }
+    if (local == GVRT_OK && rank_ == 0 && hipMalloc(&img_buf, (size_t)4 * width_ * height_) != hipSuccess) {
+        img_buf = nullptr;
+        local = fail(GVRT_ERR_OOM, "calibration frame");
+    }
+    if (agree(local) != GVRT_OK) {
+        if (d) (void)hipFree(d);
+        if (img_buf) (void)hipFree(img_buf);
+        return st_;
+    }
+    std::string why;
+    if (rank_ == 0) {
+        // each view alone, twice: the second launch is cost-ordered (bench.py view_cost_calibration)
+        std::vector<double> msg(nv + 1, 0.0);
+        gvrt_image img{img_buf, nullptr, nullptr, nullptr, 1, 0};
+        bool ok = true;
+        for (size_t v = 0; v < nv && ok; ++v) {
+            for (int k = 0; k < 2 && ok; ++k)
+                ok = gvrt_render_async(h, &app_.params, rig_[v].data(), rig_proj_.data(), width_, height_, 1, nullptr, 0,
+                                       &img) == GVRT_OK &&
+                     gvrt_sync(h) == GVRT_OK;
+            if (ok) msg[v + 1] = app_.stats().render_ms;
+        }
+        if (!ok) why = std::string("calibration render: ") + gvrt_last_error(h);
+        msg[0] = ok ? 0.0 : 1.0;
+        if (hipMemcpy(d, msg.data(), sizeof(double) * (nv + 1), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipMemset(d, 0xFF, sizeof(double));  // best effort: a NaN status word reads as a failure
+            if (ok) why = "cost upload";
+        }
+        (void)hipFree(img_buf);
+    }
+    if (rccl(ncclBroadcast(d, d, nv + 1, ncclFloat64, 0, comm_, stream_), "ncclBroadcast")) {
+        (void)hipFree(d);
+        return st_;
+    }
+    std::vector<double> msg(nv + 1, 1.0);
+    gvrt_status s = GVRT_OK;
+    if (hipStreamSynchronize(stream_) != hipSuccess) s = fail(GVRT_ERR_HIP, "broadcast sync");
+    if (s == GVRT_OK && hipMemcpy(msg.data(), d, sizeof(double) * (nv + 1), hipMemcpyDeviceToHost) != hipSuccess)
+        s = fail(GVRT_ERR_HIP, "cost readback");
+    (void)hipFree(d);
+    if (s == GVRT_OK && !(msg[0] == 0.0))
+        s = fail(GVRT_ERR_STATE, "view-cost calibration failed on rank 0" + (why.empty() ? std::string() : ": " + why));
+    if (s == GVRT_OK) std::copy(msg.begin() + 1, msg.end(), costs->begin());
     return s;
 }
 
 SplitFrame::SplitFrame(GvrtApp& app, int rank, int world, const ncclUniqueId& id, uint32_t width, uint32_t height,
-                       Layout layout)
-    : app_(app), rank_(rank), world_(world), width_(width), height_(height) {
+                       Layout layout, const std::vector<gm::mat4>* rig, const gm::mat4* rig_proj_inv)
+    : app_(app), rank_(rank), world_(world), width_(width), height_(height), layout_(layout) {
     if (world < 1 || rank < 0 || rank >= world) {
         fail(GVRT_ERR_INVALID_ARG, "rank must be in [0, world)");
+        return;
+    }
+    // (argument errors are the same on every rank: refused before the communicator exists)
+    if (layout == VIEWS && (!rig || !rig_proj_inv || rig->empty() || rig->size() > 255)) {
+        fail(GVRT_ERR_INVALID_ARG, "the VIEWS layout needs a rig of 1..255 views and its projection inverse");
         return;
     }
     if (hipSetDevice(app.device.ordinal) != hipSuccess) {
@@ -151,43 +293,59 @@ SplitFrame::SplitFrame(GvrtApp& app, int rank, int world, const ncclUniqueId& id
         return;
     }
     if (rccl(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank")) return;
+    // from here on every failure is agreed on (agree) or travels in a broadcast's status word: no rank leaves a
+    // collective its peers have entered
+    gvrt_status local = GVRT_OK;
     if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
+        // the collectives below need a stream: without one this rank cannot take part
         fail(GVRT_ERR_HIP, "hipStreamCreateWithFlags");
+        stream_ = nullptr;
+        abort_comm();
         return;
     }
     // the handle renders (and unpacks) on the exchange's stream: render -> send/recv -> scatter in stream order
-    if (gvrt_set_stream(app.handle(), stream_) != GVRT_OK) {
-        fail(GVRT_ERR_HIP, std::string("gvrt_set_stream: ") + gvrt_last_error(app.handle()));
-        return;
-    }
-    if (layout == COST_BANDS) {
-        std::vector<uint8_t> classes;
-        if (cost_classes(&classes) != GVRT_OK) return;
-        all_tiles_ = band_tiles(width, height, world, classes.data());
+    if (gvrt_set_stream(app.handle(), stream_) != GVRT_OK)
+        local = fail(GVRT_ERR_HIP, std::string("gvrt_set_stream: ") + gvrt_last_error(app.handle()));
+    if (agree(local) != GVRT_OK) return;
+    size_t part_bytes = 0;
+    if (layout == VIEWS) {
+        rig_ = *rig;
+        rig_proj_ = *rig_proj_inv;
+        if (view_costs_bcast(&view_costs_) != GVRT_OK) return;
+        views_ = balanced_views(view_costs_, world);
+        for (uint32_t v : views_[rank])
+            my_vi_.insert(my_vi_.end(), rig_[v].data(), rig_[v].data() + 16);
+        part_bytes = (size_t)views_[rank].size() * 4 * width * height;
     } else {
-        for (int r = 0; r < world; ++r) all_tiles_.push_back(rank_tiles(width, height, 1, r, world));
+        if (layout == COST_BANDS) {
+            std::vector<uint8_t> classes;
+            if (cost_classes(&classes) != GVRT_OK) return;
+            all_tiles_ = band_tiles(width, height, world, classes.data());
+        } else {
+            for (int r = 0; r < world; ++r) all_tiles_.push_back(rank_tiles(width, height, 1, r, world));
+        }
+        tiles_ = all_tiles_[rank];
+        part_bytes = (size_t)tiles_.size() * 256;
     }
-    tiles_ = all_tiles_[rank];
-    if (hipMalloc(&d_part_, std::max<size_t>(16, (size_t)tiles_.size() * 256)) != hipSuccess) {
+    if (hipMalloc(&d_part_, std::max<size_t>(16, part_bytes)) != hipSuccess) {
         d_part_ = nullptr;
-        fail(GVRT_ERR_OOM, "part buffer");
-        return;
+        local = fail(GVRT_ERR_OOM, "part buffer");
     }
-    if (rank == 0) {
+    if (local == GVRT_OK && rank == 0 && layout != VIEWS) {
         d_recv_.assign(world, nullptr);
-        for (int r = 0; r < world; ++r)
+        for (int r = 0; r < world && local == GVRT_OK; ++r)
             if (hipMalloc(&d_recv_[r], std::max<size_t>(16, (size_t)all_tiles_[r].size() * 256)) != hipSuccess) {
                 d_recv_[r] = nullptr;
-                fail(GVRT_ERR_OOM, "receive buffer");
-                return;
+                local = fail(GVRT_ERR_OOM, "receive buffer");
             }
     }
+    agree(local);
 }
 
 SplitFrame::~SplitFrame() {
     (void)hipSetDevice(app_.device.ordinal);
     if (stream_) (void)hipStreamSynchronize(stream_);
-    if (app_.handle()) (void)gvrt_set_stream(app_.handle(), nullptr);
+    if (app_.handle() && stream_) (void)gvrt_set_stream(app_.handle(), nullptr);
     for (void* p : d_recv_)
         if (p) (void)hipFree(p);
     if (d_part_) (void)hipFree(d_part_);
@@ -196,29 +354,66 @@ SplitFrame::~SplitFrame() {
 }
 
 gvrt_status SplitFrame::draw(void* frame) {
-    if (st_ != GVRT_OK) return st_;
-    if (rank_ == 0 && !frame) return fail(GVRT_ERR_INVALID_ARG, "rank 0 needs a frame");
+    if (st_ != GVRT_OK) {
+        abort_comm();  // a rank that cannot take part any more: its peers' exchange errors out instead of waiting
+        return st_;
+    }
+    if (rank_ == 0 && !frame) {
+        // refused before the exchange: the peers are told through the aborted communicator
+        fail(GVRT_ERR_INVALID_ARG, "rank 0 needs a frame");
+        abort_comm();
+        return st_;
+    }
     gvrt_handle h = app_.handle();
-    // this rank's tiles, tile-packed, queued on the stream (gvrt_render_async: no host wait)
-    gvrt_image img{d_part_, nullptr, nullptr, nullptr, 1, 1};
-    if (gvrt_render_async(h, &app_.params, app_.uniformDataDynamic.viewInverse.data(),
-                          app_.uniformDataDynamic.projInverse.data(), width_, height_, 1, tiles_.data(), tiles_.size(),
-                          &img) != GVRT_OK)
-        return fail(GVRT_ERR_HIP, std::string("gvrt_render_async: ") + gvrt_last_error(h));
-    // the exchange: every rank's part to rank 0, one group (rank 0 also sends its own part to itself)
+    const size_t view_bytes = (size_t)4 * width_ * height_;
+    // this rank's part, queued on the stream (gvrt_render_async: no host wait): its tiles tile-packed, or its views
+    // in one batched launch ([view][H][W][4])
+    gvrt_status local = GVRT_OK;
+    gvrt_image img{d_part_, nullptr, nullptr, nullptr, 1, layout_ == VIEWS ? 0u : 1u};
+    gvrt_status rs;
+    if (layout_ == VIEWS)
+        rs = views_[rank_].empty() ? GVRT_OK
+                                   : gvrt_render_async(h, &app_.params, my_vi_.data(), rig_proj_.data(), width_, height_,
+                                                       (uint32_t)views_[rank_].size(), nullptr, 0, &img);
+    else
+        rs = gvrt_render_async(h, &app_.params, app_.uniformDataDynamic.viewInverse.data(),
+                               app_.uniformDataDynamic.projInverse.data(), width_, height_, 1, tiles_.data(),
+                               tiles_.size(), &img);
+    if (rs != GVRT_OK) local = fail(GVRT_ERR_HIP, std::string("gvrt_render_async: ") + gvrt_last_error(h));
+    // the exchange, entered even after a failed render (the part then holds a stale frame): every rank's part to
+    // rank 0 in one group, exact sizes (rank 0 also sends its own part to itself); views land in their frame slots
     if (rccl(ncclGroupStart(), "ncclGroupStart")) return st_;
-    if (rccl(ncclSend(d_part_, tiles_.size() * 256, ncclUint8, 0, comm_, stream_), "ncclSend")) return st_;
-    if (rank_ == 0)
-        for (int r = 0; r < world_; ++r)
-            if (rccl(ncclRecv(d_recv_[r], all_tiles_[r].size() * 256, ncclUint8, r, comm_, stream_), "ncclRecv"))
+    if (layout_ == VIEWS) {
+        for (size_t i = 0; i < views_[rank_].size(); ++i)
+            if (rccl(ncclSend((uint8_t*)d_part_ + i * view_bytes, view_bytes, ncclUint8, 0, comm_, stream_), "ncclSend"))
                 return st_;
+        if (rank_ == 0)
+            for (int r = 0; r < world_; ++r)
+                for (uint32_t v : views_[r])
+                    if (rccl(ncclRecv((uint8_t*)frame + v * view_bytes, view_bytes, ncclUint8, r, comm_, stream_),
+                             "ncclRecv"))
+                        return st_;
+    } else {
+        if (rccl(ncclSend(d_part_, tiles_.size() * 256, ncclUint8, 0, comm_, stream_), "ncclSend")) return st_;
+        if (rank_ == 0)
+            for (int r = 0; r < world_; ++r)
+                if (rccl(ncclRecv(d_recv_[r], all_tiles_[r].size() * 256, ncclUint8, r, comm_, stream_), "ncclRecv"))
+                    return st_;
+    }
     if (rccl(ncclGroupEnd(), "ncclGroupEnd")) return st_;
-    // rank 0: scatter every part into the frame, behind the receives on the same stream
-    if (rank_ == 0)
+    if (local != GVRT_OK) {
+        abort_comm();
+        return st_;
+    }
+    // rank 0, tile layouts: scatter every part into the frame, behind the receives on the same stream
+    if (rank_ == 0 && layout_ != VIEWS)
         for (int r = 0; r < world_; ++r)
             if (gvrt_unpack_tiles_rgba8(h, d_recv_[r], all_tiles_[r].data(), all_tiles_[r].size(), width_, height_, 1,
-                                        frame) != GVRT_OK)
-                return fail(GVRT_ERR_HIP, std::string("gvrt_unpack_tiles_rgba8: ") + gvrt_last_error(h));
+                                        frame) != GVRT_OK) {
+                fail(GVRT_ERR_HIP, std::string("gvrt_unpack_tiles_rgba8: ") + gvrt_last_error(h));
+                abort_comm();
+                return st_;
+            }
     return GVRT_OK;
 }
 

@@ -10,8 +10,17 @@
 // renders on it, gvrt_set_stream), so a frame costs no host round trip.  The reference has no multi-GPU path:
 // this replaces the single vkCmdTraceRaysKHR of buildCommandBuffer (VulkanFullRT.cpp:1217-1230) by N of them.
 //
+// Config 5 (the light field on N GPUs, VulkanFullRT.cpp:1900-1976 computeGaussianLightField) splits whole views
+// instead: layout VIEWS assigns the views of a camera rig to the ranks by cost (balanced_views, bit for bit the
+// Python layer's dist.balanced_views), each rank renders its views in one batched launch, and every view goes to
+// rank 0 whole, straight into its slot of the [view][H][W][4] frame.
+//
 // Errors are statuses: an RCCL failure is GVRT_ERR_RCCL (include/gvrt.h), a HIP failure GVRT_ERR_HIP; error()
-// has the text.
+// has the text.  No failure leaves a peer waiting in a collective: set-up failures are agreed on by an all-reduce
+// of every rank's status before anything rank-specific, rank 0's calibration result travels with a status word in
+// the one broadcast every rank always enters, and a rank that fails inside draw() still enters that frame's
+// exchange (sending what its part buffer holds) and aborts the communicator before it returns the failure, so the
+// peers' next exchange errors out instead of waiting.
 #pragma once
 #include <rccl/rccl.h>
 
@@ -32,6 +41,11 @@ std::vector<gvrt_tile> rank_tiles(uint32_t width, uint32_t height, uint32_t ncam
 std::vector<std::vector<gvrt_tile>> band_tiles(uint32_t width, uint32_t height, int world, const uint8_t* classes,
                                                uint32_t block = 8);
 
+// Cost-weighted view assignment (dist.balanced_views): every rank gets floor or ceil(views / world) views, placed
+// costliest first on the least-loaded rank with room (ties: lower rank, lower view index); each rank's views in
+// increasing index
+std::vector<std::vector<uint32_t>> balanced_views(const std::vector<double>& costs, int world);
+
 // Rendezvous of the communicator: rank 0 creates the RCCL unique id and writes it to `path` (written to a
 // temporary name and renamed, so a reader never sees half a file); every other rank waits for the file (up to
 // timeout_s seconds).  Returns GVRT_OK or GVRT_ERR_RCCL / GVRT_ERR_IO with the text in *err.
@@ -40,13 +54,17 @@ gvrt_status rccl_rendezvous(const std::string& path, int rank, ncclUniqueId* id,
 
 class SplitFrame {
   public:
-    enum Layout { BLOCKS = 0, COST_BANDS = 1 };
+    enum Layout { BLOCKS = 0, COST_BANDS = 1, VIEWS = 2 };
     // ncclCommInitRank(world, id, rank) on the app's device; the app's handle then renders on this object's stream.
     // COST_BANDS: rank 0 renders the app's current frame twice and reads its per-tile cost classes
     // (gvrt_read_tile_costs), one ncclBroadcast hands them to every rank, and all cut the same bands (band_tiles);
-    // BLOCKS: 64x64-pixel blocks round-robin (rank_tiles)
+    // BLOCKS: 64x64-pixel blocks round-robin (rank_tiles);
+    // VIEWS: the views of `rig` (view inverses, shared projection inverse) split over the ranks: rank 0 renders
+    // each view alone twice and times the second (cost-ordered) launch, one ncclBroadcast hands the costs to every
+    // rank, and all compute the same balanced_views assignment
     SplitFrame(GvrtApp& app, int rank, int world, const ncclUniqueId& id, uint32_t width, uint32_t height,
-               Layout layout = COST_BANDS);
+               Layout layout = COST_BANDS, const std::vector<gm::mat4>* rig = nullptr,
+               const gm::mat4* rig_proj_inv = nullptr);
     ~SplitFrame();
     SplitFrame(const SplitFrame&) = delete;
     SplitFrame& operator=(const SplitFrame&) = delete;
@@ -56,18 +74,25 @@ class SplitFrame {
 
     // one frame with the app's uniformDataDynamic: this rank's tiles rendered tile-packed, gathered to rank 0 and
     // scattered into `frame` (device rgba8 [H][W][4], rank 0 only; ignored elsewhere).  Queued on the stream.
+    // VIEWS: this rank's views of the rig, each sent whole into frame's view slot (device rgba8 [views][H][W][4]).
     gvrt_status draw(void* frame);
     gvrt_status sync();  // waits for every queued frame on this rank
 
     int rank() const { return rank_; }
     int world() const { return world_; }
     const std::vector<gvrt_tile>& tiles() const { return tiles_; }
+    const std::vector<std::vector<uint32_t>>& views() const { return views_; }  // VIEWS: every rank's views
+    const std::vector<double>& view_costs() const { return view_costs_; }    // VIEWS: calibration kernel ms
     double lastKernelMs() const;  // mean kernel time of the frames completed by the last sync (gvrt_stats)
 
   private:
     gvrt_status fail(gvrt_status s, const std::string& m);
     gvrt_status rccl(ncclResult_t r, const char* what);
-    gvrt_status cost_classes(std::vector<uint8_t>* classes);  // rank 0 measures, every rank receives
+    // rank 0 measures, every rank receives (one broadcast of a status word and the payload, always entered)
+    gvrt_status cost_classes(std::vector<uint8_t>* classes);
+    gvrt_status view_costs_bcast(std::vector<double>* costs);
+    gvrt_status agree(gvrt_status local);  // every rank's set-up status, all-reduced: the worst one everywhere
+    void abort_comm();                     // a failure inside draw(): peers' next exchange errors out
 
     GvrtApp& app_;
     int rank_, world_;
@@ -80,6 +105,12 @@ class SplitFrame {
     std::vector<std::vector<gvrt_tile>> all_tiles_;  // every rank's (rank 0 scatters with them)
     void* d_part_ = nullptr;                         // this rank's packed part: tiles * 64 px * 4 B
     std::vector<void*> d_recv_;                      // rank 0: one receive buffer per rank
+    Layout layout_ = COST_BANDS;
+    std::vector<gm::mat4> rig_;                       // VIEWS: the rig's view inverses
+    gm::mat4 rig_proj_{};
+    std::vector<std::vector<uint32_t>> views_;        // VIEWS: every rank's views (balanced_views)
+    std::vector<double> view_costs_;
+    std::vector<float> my_vi_;                        // VIEWS: this rank's view inverses, 16 floats each
 };
 
 }  // namespace gvrt_host

@@ -42,8 +42,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table
-# VALU issue: 256 CUs x 4 SIMDs x 2.4 GHz, one wave64 VALU instruction per 2 cycles per SIMD (MI355X_MICROARCH.md)
-VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2
+# VALU issue: 256 CUs x 4 SIMD-32s, a wave64 VALU instruction occupies its SIMD for 2 cycles (MI355X_MICROARCH.md);
+# the clock is the one measured over the dispatch (GRBM_GUI_ACTIVE counts cycles on each of the 8 XCDs)
+N_SIMD = 256 * 4
+N_XCD = 8
 
 
 def parse():
@@ -80,6 +82,10 @@ def parse():
     ap.add_argument("--option", action="append", default=[], metavar="NAME=0|1",
                     help="per-handle tuning switch (gvrt_set_option; names in _lib.OPTIONS), for same-box A/B runs; "
                          "none of them changes an image")
+    ap.add_argument("--strong", default="bicycle,truck",
+                    help="N-rank runs (--gpus N > 1, or --exchange): strong-scaling sub-records of these frames "
+                         "(bicycle: the config-2 1080p frame, truck: the config-4 4K frame), each tile-split over the "
+                         "ranks in cost bands and exchanged to rank 0; 'none' to skip")
     ap.add_argument("--build", default="quality", choices=["quality", "fast"],
                     help="quality: device binned-SAH tree + SAH-optimal 4-wide collapse (the static-scene build, "
                          "as the reference's PREFER_FAST_TRACE BLAS); fast: device LBVH + greedy collapse")
@@ -137,7 +143,10 @@ def pmc_passes(args):
     if args.camera_path != "static":
         child += ["--camera-path", args.camera_path, "--orbit-step", str(args.orbit_step)]
     out = {}
-    passes = [["FETCH_SIZE"], ["WRITE_SIZE"], ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM"]]
+    # (8 SQ counters and 1 GRBM counter fit one pass; FETCH_SIZE / WRITE_SIZE need TCC passes of their own)
+    passes = [["FETCH_SIZE"], ["WRITE_SIZE"],
+              ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY",
+               "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "GRBM_GUI_ACTIVE"]]
     tmp = tempfile.mkdtemp(prefix="gvrt_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
         for i, counters in enumerate(passes):
@@ -197,6 +206,105 @@ def view_cost_calibration(r, vis, pi, W, H, params, reps=2):
             r.render_device(np.ascontiguousarray(v), pi, W, H, 1, params=params, rgba8_ptr=buf.data_ptr())
         out.append(float(r.render_ms()))
     return out
+
+
+def strong_scaling_record(gv, dist_mod, dist, r, vi, pi, W, H, params, rank, world, dev, label, steps=10, warmup=3,
+                          probes=3):
+    """One frame tile-split over every rank in cost bands, all ranks together:
+    rank 0 measures the full frame's per-tile costs (two launches; the second one's kernel time is the one-GPU
+    figure), one broadcast gives every rank the classes and the same band cuts, and the split frame runs through
+    dist.FrameExchange (exact-size point-to-point sends to rank 0, rank-0 scatter by gvrt_unpack_tiles_rgba8) --
+    pipelined for `steps` frames (barrier + sync on both sides, the max over ranks), then `probes` frames one at a
+    time with HIP events around each phase: this rank's render (kernel ms from the handle), the exchange (after a
+    barrier, so it is the transfer and not a wait for a slower rank's render) and rank 0's assembly.  Returns the
+    record on rank 0 (None elsewhere); the assembled frame is checked against rank 0's one-GPU frame."""
+    import torch
+    H8, W8 = (H + 7) // 8, (W + 7) // 8
+    classes = (tile_cost_calibration(r, vi, pi, W, H, params) if rank == 0 else np.zeros((1, H8, W8), np.uint8))
+    one_ms = r.render_ms() if rank == 0 else 0.0
+    t = torch.from_numpy(np.ascontiguousarray(classes)).to(dev)
+    dist.broadcast(t, src=0)
+    classes = t.cpu().numpy()
+    all_tiles = split_tiles(dist_mod, "cost-bands", W, H, world, classes)
+    tiles = all_tiles[rank]
+    sizes = [int(x.shape[0]) * 64 for x in all_tiles]
+    full = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev) if rank == 0 else None
+
+    def assemble(parts, _k):
+        for p, tl in zip(parts, all_tiles):
+            if tl.shape[0]:
+                r.unpack_tiles_rgba8(p.data_ptr(), tl, W, H, full.data_ptr())
+
+    ex = dist_mod.FrameExchange(dist, rank, world, sizes, (4,), torch.uint8, dev, nbuf=2, assemble=assemble)
+
+    def render_into(buf):
+        if tiles.shape[0]:
+            r.render_device(vi, pi, W, H, 1, params=params, tiles=tiles, rgba8_ptr=buf.data_ptr(), packed=True,
+                            async_=True)
+
+    for _ in range(warmup):
+        ex.step(render_into)
+    ex.drain()
+    r.sync()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ex.step(render_into)
+    ex.drain()
+    r.sync()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    ms_frame = float(el.item()) / steps * 1e3
+    pipe_kms = r.render_ms() if tiles.shape[0] else 0.0  # mean over the pipelined launches
+    # per-phase probes, one frame at a time
+    pk, px, pa = [], [], []
+    for _ in range(probes):
+        evs = {}
+
+        def mark(name):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            evs[name] = e
+
+        def barrier():
+            torch.cuda.current_stream().synchronize()
+            dist.barrier()
+
+        ex.probe(render_into, mark, barrier=barrier)
+        r.sync()
+        torch.cuda.synchronize()
+        pk.append(r.render_ms() if tiles.shape[0] else 0.0)
+        px.append(evs["posted"].elapsed_time(evs["exchanged"]))
+        pa.append(evs["exchanged"].elapsed_time(evs["assembled"]))
+    mine = torch.tensor([pipe_kms, float(np.median(pk)), float(np.median(px)), float(np.median(pa)), sizes[rank] * 4.0],
+                        dtype=torch.float64, device=dev)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    if rank != 0:
+        return None
+    per = torch.stack(allr).cpu().numpy()
+    got = hashlib.sha1(full.cpu().numpy().tobytes()).hexdigest()
+    ref = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
+    r.render_device(vi, pi, W, H, 1, params=params, rgba8_ptr=ref.data_ptr())
+    torch.cuda.synchronize()
+    one_sha = hashlib.sha1(ref.cpu().numpy().tobytes()).hexdigest()
+    return {"frame": label, "layout": "cost-bands", "ranks": world, "steps": steps,
+            "ms_per_frame": round(ms_frame, 4), "mrays": round(W * H / (ms_frame * 1e-3) / 1e6, 1),
+            "one_gpu_kernel_ms": round(one_ms, 4),
+            "tiles_per_rank": [int(x.shape[0]) for x in all_tiles],
+            "kernel_ms_per_rank": [round(float(x), 4) for x in per[:, 0]],
+            "probe_kernel_ms_per_rank": [round(float(x), 4) for x in per[:, 1]],
+            "exchange_ms_per_rank": [round(float(x), 4) for x in per[:, 2]],
+            "assemble_ms": round(float(per[0, 3]), 4),
+            "exchange_bytes": int(ex.exchange_bytes), "padded_gather_bytes_round3": int(ex.padded_gather_bytes),
+            "bytes_sent_per_rank": [int(x) for x in per[:, 4]],
+            "identical_to_one_gpu": got == one_sha, "frame_sha1": got,
+            "note": "pipelined: FrameExchange double-buffered, the exchange of frame i under the render of i+1; "
+                    "probe_*: one frame at a time, the exchange timed after a barrier (transfer only), assembly on "
+                    "rank 0 (gvrt_unpack_tiles_rgba8); rank r > 0 sends its exact part, rank 0's part stays put"}
 
 
 def rank_balance(args, r, gv, dist_mod, vi_all, pi, W, H, views, params, full_ms, reps=4, view_costs=None):
@@ -481,7 +589,7 @@ def main():
                 img = full
             else:  # view 0 in the part of the rank that rendered it
                 r0 = next(k for k, g in enumerate(all_views) if 0 in g)
-                img = ex.recv[(ex.frames - 1) % ex.nbuf][r0][all_views[r0].index(0)]
+                img = ex.parts((ex.frames - 1) % ex.nbuf)[r0][all_views[r0].index(0)]
         else:
             img = frame if not packed else None
             if packed:  # one rank: unpack the whole frame's tiles
@@ -492,10 +600,38 @@ def main():
         torch.cuda.synchronize()
         digest = hashlib.sha1(img.cpu().numpy().tobytes()).hexdigest()
 
+    # ---- strong-scaling sub-records (N-rank runs): one frame tile-split over all ranks, every rank taking part
+    strong = []
+    if distributed and args.strong != "none":
+        for name in [x for x in args.strong.split(",") if x]:
+            if name == "bicycle" and args.config == "bicycle" and not args.ply:
+                rs, own = r, False
+            else:
+                gen_s, _, _, _ = gv.scene.CONFIGS[name]
+                rs, own = gv.Renderer(local_rank), True
+                rs.prepare(gv.scene.make(**gen_s), **bkw)
+                rs.set_stream(torch.cuda.current_stream().cuda_stream)
+            _, Ws, Hs, _ = gv.scene.CONFIGS[name]
+            vs, ps = gv.scene.mipnerf_camera(Ws, Hs)
+            rec = strong_scaling_record(gv, dist_mod, dist, rs, np.ascontiguousarray(vs, np.float32), ps, Ws, Hs,
+                                        rs.render_params(mode=mode), rank, world, dev,
+                                        f"{name} {Ws}x{Hs} ({'config 2' if name == 'bicycle' else 'config 4'})")
+            if own:
+                rs.close()
+            if rec:
+                strong.append(rec)
+
     if rank == 0:
-        # ---- roofline: algorithmic bytes of the reference algorithm on this input (LITERAL counters)
+        # ---- roofline.  The binding resource, from the PMC passes of this command: instruction issue.  The kernel
+        # moves ~0.2 GB per launch through HBM (2-3 % of 8 TB/s) and its waves spend their lifetime issuing (~42 %),
+        # waiting on dependent scalar loads (~38 %) or ready behind other waves' issue (~20 %); the busiest unit is
+        # the SIMDs' VALU pipe: frac = 2 x VALU wave-instructions / (1024 SIMDs x the dispatch's cycles), <= 1 by
+        # construction.  roofline.logical keeps SURVEY §8d's algorithmic-bytes figure of round 1-3 (the reference
+        # algorithm's gather bytes, from the LITERAL counters: above 1 on scenes where packet traversal shares most
+        # gathers across a wave's 64 rays, so it is no bound).
         roof = None
         lit_stats = None
+        logical = None
         vi = frame_vi[0]  # the frame-0 camera (the static headline's) for the counters and the CPU baseline
         if not args.no_stats:
             r.set_stats(True)
@@ -506,25 +642,49 @@ def main():
             bytes_per_launch = (48.0 * lit_stats["crossings"] + 192.0 * lit_stats["accepted"] + 4.0 * rays1) * (
                 rays_per_rank / rays1)
             achieved = bytes_per_launch / (kern_avg * 1e-3) / 1e9
-            traffic = None
-            if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
-                # FETCH_SIZE in KiB, half-counted on gfx950 (x2); WRITE_SIZE in KiB (MI355X_MICROARCH.md, HBM)
-                traffic = pmc["FETCH_SIZE"] * 1024 * 2 + pmc["WRITE_SIZE"] * 1024
-            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                    "algorithmic_bytes_per_launch": bytes_per_launch,
-                    "kernel_ms_avg": round(kern_avg, 4), "kernel": "k_render<FAST,K=24,packed>"}
+            logical = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(achieved / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_launch": bytes_per_launch,
+                       "note": "SURVEY §8d: sum over rays of 48 B per crossing + 192 B per accepted crossing + 4 B, the "
+                               "reference algorithm's counters; not a bound (packet traversal shares the gathers)"}
+        traffic = None
+        if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+            # FETCH_SIZE in KiB, half-counted on gfx950 (x2); WRITE_SIZE in KiB (MI355X_MICROARCH.md, HBM)
+            traffic = pmc["FETCH_SIZE"] * 1024 * 2 + pmc["WRITE_SIZE"] * 1024
+        kern = "k_render<FAST,K=24,packed>" if args.mode == "fast" else "k_render<LITERAL,K=16>"
+        if pmc and "SQ_INSTS_VALU" in pmc and pmc.get("GRBM_GUI_ACTIVE"):
+            cyc = pmc["GRBM_GUI_ACTIVE"] / N_XCD  # shader cycles of the dispatch
+            clock = cyc / (kern_avg * 1e-3)
+            rate = pmc["SQ_INSTS_VALU"] / (kern_avg * 1e-3)
+            peak = N_SIMD * clock / 2.0
+            waves = max(pmc.get("SQ_WAVES", 1), 1)
+            roof = {"bound": "issue", "achieved": rate, "peak": peak, "unit": "VALU wave-instr/s",
+                    "frac": round(2.0 * pmc["SQ_INSTS_VALU"] / (N_SIMD * cyc), 4), "traffic": traffic,
+                    "binding_unit": "SIMD VALU issue: a wave64 VALU instruction holds a SIMD-32 for 2 cycles; peak = "
+                                    "1024 SIMDs x the dispatch's clock (GRBM_GUI_ACTIVE / 8 XCDs / kernel time) / 2",
+                    "clock_ghz": round(clock / 1e9, 4),
+                    "valu_per_wave": pmc["SQ_INSTS_VALU"] / waves,
+                    "salu_per_wave": pmc.get("SQ_INSTS_SALU", 0) / waves,
+                    "smem_per_wave": pmc.get("SQ_INSTS_SMEM", 0) / waves}
+            if pmc.get("SQ_WAVE_CYCLES"):
+                wc = pmc["SQ_WAVE_CYCLES"]
+                roof["wave_cycles"] = {"issuing": round(pmc.get("SQ_ACTIVE_INST_ANY", 0) / wc, 4),
+                                       "waiting_on_memory": round(pmc.get("SQ_WAIT_ANY", 0) / wc, 4),
+                                       "ready_not_issued": round(pmc.get("SQ_WAIT_INST_ANY", 0) / wc, 4)}
+        elif logical:  # no PMC passes (--no-pmc or rocprofv3 missing): the logical figure stands in
+            roof = {**logical, "traffic": traffic, "note": "no PMC passes: " + str((pmc or {}).get("error", "--no-pmc"))}
+        if roof is not None:
+            roof["kernel_ms_avg"] = round(kern_avg, 4)
+            roof["kernel"] = kern
+            if logical:
+                roof["logical"] = logical
+            if traffic is not None:
+                hb = traffic / (kern_avg * 1e-3) / 1e9
+                roof["hbm"] = {"achieved": round(hb, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(hb / HBM_PEAK_GBS, 5),
+                               "traffic_read_bytes": pmc["FETCH_SIZE"] * 1024 * 2,
+                               "traffic_write_bytes": pmc["WRITE_SIZE"] * 1024}
             if pmc:
                 roof["pmc"] = {k: v for k, v in pmc.items()}
-                if traffic is not None:
-                    roof["traffic_read_bytes"] = pmc["FETCH_SIZE"] * 1024 * 2
-                    roof["traffic_write_bytes"] = pmc["WRITE_SIZE"] * 1024
-                if "SQ_INSTS_VALU" in pmc:
-                    rate = pmc["SQ_INSTS_VALU"] / (kern_avg * 1e-3)
-                    roof["valu_issue"] = {"achieved": rate, "peak": VALU_PEAK_WAVE_INSTR, "unit": "wave-instr/s",
-                                          "frac": round(rate / VALU_PEAK_WAVE_INSTR, 4),
-                                          "valu_per_wave": pmc["SQ_INSTS_VALU"] / max(pmc.get("SQ_WAVES", 1), 1),
-                                          "salu_per_wave": pmc.get("SQ_INSTS_SALU", 0) / max(pmc.get("SQ_WAVES", 1), 1)}
 
         # ---- CPU baseline (oracle restatement on the host's CPU share), PSNR vs oracle on the sample
         cpu = None
@@ -656,6 +816,8 @@ def main():
         }
         if balance:
             result["rank_balance"] = balance
+        if strong:
+            result["strong_scaling"] = strong
         if orbit_static:
             result["orbit_same_views_static"] = orbit_static
         if host_out:

@@ -266,7 +266,11 @@ gvrt_status gvrt_get_device_buffers(gvrt_handle h, gvrt_device_buffers* out);
                                        leaves of all-leaf nodes have the boxes of their acceptance ellipsoids (for
                                        the launch's hit_min_gaussian_response / alpha_min) and particles that can
                                        never be accepted are dropped; 0: the proxy boxes */
-#define GVRT_OPT_COUNT 8u
+#define GVRT_OPT_OPTIONAL_MEM_MB 8u /* 0 (default): no limit; N > 0: the optional speed-up copies (octant and
+                                       acceptance node copies, record-origin copies) are allocated only while the
+                                       handle's device memory stays within N MiB; a copy that does not fit (or
+                                       whose hipMalloc fails) is left out and launches run without it */
+#define GVRT_OPT_COUNT 9u
 gvrt_status gvrt_set_option(gvrt_handle h, uint32_t option, int64_t value);
 gvrt_status gvrt_get_option(gvrt_handle h, uint32_t option, int64_t* value);
 

@@ -206,9 +206,47 @@ struct Scene {
 };
 
 // gaussianfunctions.glsl:153-229 processHit (SURFEL_PRIMITIVE false, ENABLE_NORMALS false)
+// cond (parity accounting only): the relative change of gres per ulp of rounding in the ray or the kernel-frame
+// origin.  The line's distance from the centre, |gcrod| = |grd x gro|, is a difference of products of size |gro|,
+// so one ulp moves it by ~ |gro| 2^-24, and ln gres = S grayDist^2 = S |gcrod|^4 moves by 4 |ln gres| times its
+// relative change: cond = 4 |ln gres| |gro| / |gcrod| 2^-24.  A particle far away in kernel units (|gro| of
+// several hundred: small and distant) makes the response ill-conditioned, and two float evaluations of it (the
+// GPU's v_rsq / FMA order, this CPU's) can then differ by more than the fixed THR_EPS.
 struct HitEval {
     float gres, galpha;
+    float cond = 0.0f;
 };
+constexpr float ULP = 5.9604645e-8f;  // 2^-24
+
+// Parity accounting only (oracle_params::perturb_ulps, tests/test_oracle_kat.py): "another float evaluation" of the
+// same ray -- the ray direction and each particle's kernel-frame origin and direction moved by a pseudo-random
+// whole number of ulps in [-g_jig_ulps, g_jig_ulps], seeded by (ray, particle) so that every evaluation of one
+// crossing (clip, insert-time and composite-time response) sees the same perturbation, as on the GPU.
+thread_local uint32_t g_jig_ulps = 0;
+thread_local uint64_t g_jig_ray = 0;
+inline uint64_t mix64(uint64_t h) {
+    h ^= h >> 29;
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 32;
+    return h;
+}
+inline float jigf(float x, uint64_t& h) {
+    h = mix64(h + 0x9E3779B97F4A7C15ull);
+    const int32_t k = (int32_t)(h % (2 * g_jig_ulps + 1)) - (int32_t)g_jig_ulps;
+    for (int32_t i = 0; i < std::abs(k); ++i) x = std::nextafter(x, k > 0 ? INFINITY : -INFINITY);
+    return x;
+}
+inline V3 jig3(V3 v, uint64_t& h) {
+    if (!g_jig_ulps) return v;
+    const float x = jigf(v.x, h), y = jigf(v.y, h), z = jigf(v.z, h);
+    return v3(x, y, z);
+}
+inline uint64_t jig_seed(uint32_t idx) { return mix64(g_jig_ray * 0x100000001B3ull + idx + 1); }
+inline float responseCond(float grayDist, float gro_len) {
+    // |ln gres| = |S| grayDist^2 and |gcrod| = sqrt(grayDist)
+    if (!(grayDist > 0.0f)) return 0.0f;
+    return 4.0f * 0.0555555555556f * grayDist * std::sqrt(grayDist) * gro_len * ULP;
+}
 inline HitEval evalResponse(const Scene& s, uint32_t idx, V3 o, V3 d) {
     const float* rec = s.density + 12ull * idx;  // fetchParticleDensity :89-101
     const V3 pos = v3(rec[0], rec[1], rec[2]);
@@ -218,15 +256,17 @@ inline HitEval evalResponse(const Scene& s, uint32_t idx, V3 o, V3 d) {
     const V3 giscl = v3(1 / scl.x, 1 / scl.y, 1 / scl.z);
     const V3 gposc = o - pos;
     const V3 gposcr = mul(R, gposc);
-    const V3 gro = giscl * gposcr;
+    uint64_t jh = jig_seed(idx);
+    const V3 gro = jig3(giscl * gposcr, jh);
     const V3 rayDirR = mul(R, d);
-    const V3 grdu = giscl * rayDirR;
+    const V3 grdu = jig3(giscl * rayDirR, jh);
     const V3 grd = safeNormalize(grdu);
     const V3 gcrod = cross(grd, gro);
     const float grayDist = dot(gcrod, gcrod);
     HitEval h;
     h.gres = particleResponse(grayDist);
     h.galpha = std::min(0.99f, h.gres * dens);
+    h.cond = responseCond(grayDist, length(gro));
     return h;
 }
 
@@ -246,16 +286,17 @@ bool processHit(const Scene& s, V3 o, V3 d, uint32_t idx, float minKernelDensity
     const V3 giscl = v3(1 / scl.x, 1 / scl.y, 1 / scl.z);
     const V3 gposc = o - pos;
     const V3 gposcr = mul(R, gposc);
-    const V3 gro = giscl * gposcr;
+    uint64_t jh = jig_seed(idx);
+    const V3 gro = jig3(giscl * gposcr, jh);
     const V3 rayDirR = mul(R, d);
-    const V3 grdu = giscl * rayDirR;
+    const V3 grdu = jig3(giscl * rayDirR, jh);
     const V3 grd = safeNormalize(grdu);
     const V3 gcrod = cross(grd, gro);
     const float grayDist = dot(gcrod, gcrod);
     const float gres = particleResponse(grayDist);
     const float galpha = std::min(0.99f, gres * dens);
     const bool acceptHit = (gres > minKernelDensity) && (galpha > minAlpha);
-    if (eval) *eval = HitEval{gres, galpha};
+    if (eval) *eval = HitEval{gres, galpha, responseCond(grayDist, length(gro))};
     if (acceptHit) {
         const float weight = galpha * st.T;
         const V3 grds = scl * grd * dot(grd, -1.0f * gro);
@@ -287,6 +328,17 @@ float radianceMax(const Scene& s, uint32_t idx, V3 d, uint32_t sphEvalDegree) {
 // Thresholds of the parity accounting (oracle/oracle.py THR_EPS, PAIR_EPS, BOUND_EPS must equal these:
 // oracle_flag_eps, tests/test_oracle_kat.py)
 constexpr float FLAG_THR_EPS = 1e-4f, FLAG_PAIR_EPS = 2e-6f, FLAG_BOUND_EPS = 1e-5f;
+// Conditioning-aware margins (unflagged rays beyond 1e-4 were all threshold or pair decisions of
+// ill-conditioned crossings).  A decision is flagged when it lies within its fixed epsilon or within FLAG_COND_ULPS
+// ulps of rounding of its inputs, whichever is larger: a response threshold within FLAG_COND_ULPS x cond (HitEval),
+// the transmittance within the summed relative error of its factors, two crossings' t within FLAG_COND_ULPS x the
+// sum of their t conditioning (Hit::kt).  Two independent float evaluations of the same crossing (the GPU's and this
+// one) differ by up to ~3 cond (measured, scripts/parity_outliers.py), and the ray direction itself by up to 3 ulps.
+// (the default; oracle_params::flag_cond_ulps overrides it per call, 0 giving round 3's fixed margins)
+constexpr float FLAG_COND_ULPS = 6.0f;
+// margin columns stay comparable to the fixed epsilons: a distance r against an uncertainty max(eps, u) is stored as
+// r * eps / max(eps, u), so "r < max(eps, u)" reads "stored < eps" (oracle.ambiguous is unchanged)
+inline float normMargin(float r, float eps, float unc) { return r * eps / std::max(eps, unc); }
 
 // ---------------------------------------------------------------- CPU BVH over proxies
 struct BNode {
@@ -422,24 +474,45 @@ const V3 SLAB_N[10] = {{1, 1, 1},     {1, 1, -1},     {1, -1, 1},    {-1, 1, 1},
                        {0, PHI, -IPHI}, {IPHI, 0, PHI}, {-IPHI, 0, PHI}, {PHI, IPHI, 0}, {PHI, -IPHI, 0}};
 const float SQRT3 = 1.7320508075688772f;
 
-inline bool icosaCross(const Scene& s, uint32_t idx, V3 o, V3 d, float& tin, float& tout) {
+// kin / kout (parity accounting): the relative t uncertainty per ulp of the entry / exit crossing.  With
+// t = (+-h - n.ok) / (n.dk), one ulp of rounding in ok, dk or the ray moves t by ~ (|n||ok| + |t||n||dk|) 2^-24 /
+// |n.dk|: about 2^-24 / cos(theta) relative, theta the angle between the ray and the face it crosses, which grows
+// without bound for a face crossed at grazing incidence.
+inline bool icosaCross(const Scene& s, uint32_t idx, V3 o, V3 d, float& tin, float& tout, float* kin = nullptr,
+                       float* kout = nullptr) {
     const float* rec = s.density + 12ull * idx;
     const V3 pos = v3(rec[0], rec[1], rec[2]);
     const M3 R = quaternionWXYZToMatrix(rec + 4);
     const V3 giscl = v3(1 / rec[8], 1 / rec[9], 1 / rec[10]);
-    const V3 ok = giscl * mul(R, o - pos);
-    const V3 dk = giscl * mul(R, d);
+    uint64_t jh = jig_seed(idx);
+    const V3 ok = jig3(giscl * mul(R, o - pos), jh);
+    const V3 dk = jig3(giscl * mul(R, d), jh);
     const float h = s.kS[idx] * SQRT3;
     float tn = -INFINITY, tf = INFINITY;
+    int jn = -1, jf = -1;
     for (int j = 0; j < 10; ++j) {
         const float a = dot(SLAB_N[j], ok), b = dot(SLAB_N[j], dk);
         const float ib = 1.0f / b;
         const float t1 = (-h - a) * ib, t2 = (h - a) * ib;
-        tn = std::fmax(tn, std::fmin(t1, t2));
-        tf = std::fmin(tf, std::fmax(t1, t2));
+        const float lo = std::fmin(t1, t2), hi = std::fmax(t1, t2);
+        if (lo > tn) jn = j;
+        if (hi < tf) jf = j;
+        tn = std::fmax(tn, lo);
+        tf = std::fmin(tf, hi);
     }
     tin = tn;
     tout = tf;
+    if (kin && kout) {
+        const float okl = length(ok), dkl = length(dk);
+        auto kap = [&](int j, float t) {
+            if (j < 0) return 0.0f;
+            const float nl = length(SLAB_N[j]), b = std::fabs(dot(SLAB_N[j], dk));
+            if (!(b > 0.0f) || !(std::fabs(t) > 0.0f)) return 1.0f;
+            return std::min(1.0f, nl * (okl + std::fabs(t) * dkl) / (b * std::fabs(t)) * ULP);
+        };
+        *kin = kap(jn, tn);
+        *kout = kap(jf, tf);
+    }
     return tn <= tf;
 }
 
@@ -465,15 +538,21 @@ typedef struct {
     float kernel_min_response;
     uint32_t kernel_opts;
     float kernel_degree;
+    // parity accounting only (tests/test_oracle_kat.py): every ray's origin and direction components moved by a
+    // pseudo-random whole number of ulps in [-perturb_ulps, perturb_ulps] (seeded by the ray index), the size of the
+    // differences between two float evaluations of the ray (the GPU's ray generation differs by up to 3 ulps)
+    uint32_t perturb_ulps;
+    float flag_cond_ulps;  // conditioning factor of the margins (FLAG_COND_ULPS; 0: the fixed epsilons alone)
 } oracle_params;
 
 int oracle_version(void) { return 4; }
 
 // the parity accounting's flag thresholds (oracle.py THR_EPS, PAIR_EPS, BOUND_EPS)
-void oracle_flag_eps(float* out3) {
-    out3[0] = FLAG_THR_EPS;
-    out3[1] = FLAG_PAIR_EPS;
-    out3[2] = FLAG_BOUND_EPS;
+void oracle_flag_eps(float* out4) {
+    out4[0] = FLAG_THR_EPS;
+    out4[1] = FLAG_PAIR_EPS;
+    out4[2] = FLAG_BOUND_EPS;
+    out4[3] = FLAG_COND_ULPS;
 }
 
 // particlePrimitives.comp:112-215, with deterministic compaction (saveIdx = rank among
@@ -573,17 +652,20 @@ static void genRay(const float* viewInv, const float* projInv, uint32_t x, uint3
 struct Hit {
     uint32_t id;
     float t;
+    float kt = 0.0f;  // parity accounting: relative change of t per ulp of rounding (icosaCross); 0 for triangles
 };
 
 // debugging aid: when set (single-threaded trace of one ray), every processed crossing is appended as
 // {id, t, gres, galpha, T after, accepted, round}
 static thread_local std::vector<float>* g_trace = nullptr;
 
-// The per-ray ray-march: particleRendering.comp:117-191 (RQ) / raygen.rgen:303-383 (RT).
+// The per-ray ray-march: particleRendering.comp:117-191 (RQ) / raygen.rgen:113-193 (RT).
 // out_stats[3*r] = processed crossings (X_r), [3r+1] = accepted (A_r), [3r+2] = rounds.
 // out_margin[4*r .. 4*r+3] (optional; parity accounting, not part of the reference algorithm): how
 // close the ray came to a decision that a few-ulp different float evaluation (GPU exp / rsqrt / rcp,
-// FMA contraction) could take the other way.
+// FMA contraction) could take the other way.  Columns 0-2 are normalised to their fixed epsilon: a distance r
+// against the decision's uncertainty max(eps, flag_cond_ulps x its conditioning) is stored as r x eps /
+// max(eps, uncertainty) (normMargin), so "stored < eps" means "within the uncertainty".
 //   [0] relative distance to a threshold: |gres/hitMin - 1| and |galpha/alphaMin - 1| of every processed
 //       crossing, |T/minTransmittance - 1| after every accepted one;
 //   [1] relative t gap |t_i - t_j| / |t_i| between consecutive accepted crossings (their composite
@@ -680,6 +762,7 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
 
     const uint64_t nrays_full = (uint64_t)W * H * ncams;
     const uint64_t nwork = subset ? nsubset : nrays_full;
+    const float CU = P->flag_cond_ulps >= 0.0f ? P->flag_cond_ulps : FLAG_COND_ULPS;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #pragma omp parallel for schedule(dynamic, 64)
@@ -691,6 +774,12 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
         const uint32_t py = rem / W, px = rem % W;
         V3 o, d;
         genRay(viewInverse + 16ull * cam, projInverse, px, py, W, H, P->pixel_offset, o, d);
+        g_jig_ulps = P->perturb_ulps;
+        g_jig_ray = r;
+        if (g_jig_ulps) {
+            uint64_t h = mix64(r + 0x1234567ull);
+            d = jig3(d, h);
+        }
         if (out_ray_dirs) {
             uint64_t di = P->ray_dirs_layout == 1 ? ((uint64_t)cam * W * H + (uint64_t)px * H + py) : r;
             if (subset) di = w;
@@ -711,6 +800,10 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
         float last = std::max(0.0f, tminb - EPS_T);
         Hit kb[MAX_HIT_PER_TRACE];
         float m_thr = INFINITY, m_t = INFINITY, m_b = INFINITY, prev_t = NAN, prev_acc_t = NAN;
+        // t conditioning of the previous processed / accepted crossing, and the relative uncertainty of T (the summed
+        // relative errors of its factors 1 - alpha_j: alpha_j / (1 - alpha_j) x FLAG_COND_ULPS x cond_j, plus one
+        // rounding per factor)
+        float prev_kt = 0.0f, prev_acc_kt = 0.0f, t_unc = 0.0f;
         // flip bound (out_margin[3]): summed T x alpha of the flagged decisions, the largest radiance channel
         // involved, and the previous accepted crossing's T before it and alpha (pair swaps)
         float fw = 0.0f, fc = 0.0f, famax = 0.0f, prev_acc_T = 0.0f, prev_acc_a = 0.0f;
@@ -736,7 +829,7 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
             for (uint32_t i = 0; i < MAX_HIT_PER_TRACE; ++i) kb[i] = Hit{INVALID_PARTICLE_ID, INFINITE_DISTANCE};
             Hit h_out{INVALID_PARTICLE_ID, INFINITE_DISTANCE};  // nearest crossing left out of a full buffer
             // ---- trace(): driver traversal + any-hit (anyhit.rahit:40-71)
-            auto anyhit = [&](uint32_t pid, float t) {
+            auto anyhit = [&](uint32_t pid, float t, float kt) {
                 const bool inRange = (P->tmin_inclusive ? t >= tmin : t > tmin) && t <= tmax;
                 if (!inRange) {
                     if (out_margin && t == last && t <= tmax &&
@@ -752,7 +845,7 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                     const HitEval he = evalResponse(s, pid, o, d);
                     if (!(he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min)) return;
                 }
-                Hit hit{pid, t};
+                Hit hit{pid, t, kt};
                 if (hit.t < kb[MAX_HIT_PER_TRACE - 1].t) {
                     for (uint32_t i = 0; i < MAX_HIT_PER_TRACE; ++i) {  // compareAndSwapHitPayloadValue
                         if (hit.t < kb[i].t) std::swap(hit, kb[i]);
@@ -789,24 +882,25 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                 for (uint32_t k = 0; k < nd.count; ++k) {
                     const uint32_t g = bvh.items[nd.left + k];
                     if (P->proxy_mode == 1) {
-                        float tin, tout;
-                        const bool crossed = icosaCross(s, g, o, d, tin, tout);
-                        if (out_margin && std::fabs(tout - tin) < 1e-5f * std::max(std::fabs(tin), std::fabs(tout))) {
+                        float tin, tout, kin = 0.0f, kout = 0.0f;
+                        const bool crossed = icosaCross(s, g, o, d, tin, tout, &kin, &kout);
+                        const float geps = std::max(FLAG_BOUND_EPS, CU * (kin + kout));
+                        if (out_margin && std::fabs(tout - tin) < geps * std::max(std::fabs(tin), std::fabs(tout))) {
                             // grazing the proxy: whether it is crossed at all is a few-ulp decision; it
                             // matters when its crossings would be composited
                             const HitEval he = evalResponse(s, g, o, d);
                             if (he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min) {
                                 const float gg = std::fabs(tout - tin) / std::max(std::fabs(tin), 1e-30f);
-                                m_b = std::min(m_b, gg);
-                                if (gg < FLAG_BOUND_EPS) {  // both crossings of the proxy
+                                m_b = std::min(m_b, normMargin(gg, FLAG_BOUND_EPS, geps));
+                                if (gg < geps) {  // both crossings of the proxy
                                     flag(T_round, he.galpha, g);
                                     flag(T_round, he.galpha, g);
                                 }
                             }
                         }
                         if (crossed) {
-                            anyhit(g, tin);
-                            anyhit(g, tout);
+                            anyhit(g, tin, kin);
+                            anyhit(g, tout, kout);
                         }
                     } else {
                         // watertight setup
@@ -825,7 +919,7 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                             const V3 p2 = v3(verts[3ull * tr[2]], verts[3ull * tr[2] + 1], verts[3ull * tr[2] + 2]);
                             float th;
                             if (rayTri(o, d, kx, ky, kz, Sx, Sy, Sz, p0, p1, p2, th))
-                                anyhit((20 * g + t) / 20, th);  // Q2: particle id = primitive / 20
+                                anyhit((20 * g + t) / 20, th, 0.0f);  // Q2: particle id = primitive / 20
                         }
                     }
                 }
@@ -839,12 +933,16 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                 return he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min;
             };
             // (which of two tied crossings makes the round changes the image only if one of them is accepted)
+            // (the uncertainty of a gap between two crossings: the larger of the fixed epsilon and their summed
+            // t conditioning)
+            auto teps = [CU](float eps, const Hit& a, const Hit& b) { return std::max(eps, CU * (a.kt + b.kt)); };
             if (out_margin && kb[MAX_HIT_PER_TRACE - 1].id != INVALID_PARTICLE_ID && h_out.id != INVALID_PARTICLE_ID &&
-                gap(kb[MAX_HIT_PER_TRACE - 1].t, h_out.t) < 1e-4f &&
+                gap(kb[MAX_HIT_PER_TRACE - 1].t, h_out.t) < teps(FLAG_BOUND_EPS, kb[MAX_HIT_PER_TRACE - 1], h_out) &&
                 (accepted(kb[MAX_HIT_PER_TRACE - 1].id) || accepted(h_out.id))) {
                 const float gg = gap(kb[MAX_HIT_PER_TRACE - 1].t, h_out.t);
-                m_b = std::min(m_b, gg);
-                if (gg < FLAG_BOUND_EPS) {
+                const float ge = teps(FLAG_BOUND_EPS, kb[MAX_HIT_PER_TRACE - 1], h_out);
+                m_b = std::min(m_b, normMargin(gg, FLAG_BOUND_EPS, ge));
+                if (gg < ge) {
                     flag(T_round, evalResponse(s, kb[MAX_HIT_PER_TRACE - 1].id, o, d).galpha,
                          kb[MAX_HIT_PER_TRACE - 1].id);
                     flag(T_round, evalResponse(s, h_out.id, o, d).galpha, h_out.id);
@@ -865,12 +963,17 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                     if (out_margin) {
                         const float r0 = std::fabs(ev.gres / P->hit_min_gaussian_response - 1.0f);
                         const float r1 = std::fabs(ev.galpha / P->alpha_min - 1.0f);
-                        m_thr = std::min(m_thr, std::min(r0, r1));
-                        if (r0 < FLAG_THR_EPS || r1 < FLAG_THR_EPS) flag(T_before, ev.galpha, h.id);
+                        // both thresholds see gres's relative error (galpha = gres x density below the 0.99 clamp)
+                        const float re = std::max(FLAG_THR_EPS, CU * ev.cond);
+                        m_thr = std::min(m_thr, normMargin(std::min(r0, r1), FLAG_THR_EPS, re));
+                        if (r0 < re || r1 < re) flag(T_before, ev.galpha, h.id);
                         if (acc) {
+                            if (ev.galpha < 0.99f)
+                                t_unc += ev.galpha / (1.0f - ev.galpha) * CU * ev.cond + (CU > 0.0f ? 2.0f * ULP : 0.0f);
                             const float r2 = std::fabs(st.T / P->min_transmittance - 1.0f);
-                            m_thr = std::min(m_thr, r2);
-                            if (r2 < FLAG_THR_EPS) {  // the ray may go on (or stop before this crossing)
+                            const float te = std::max(FLAG_THR_EPS, t_unc);
+                            m_thr = std::min(m_thr, normMargin(r2, FLAG_THR_EPS, te));
+                            if (r2 < te) {  // the ray may go on (or stop before this crossing)
                                 const Hit nx = i + 1 < MAX_HIT_PER_TRACE ? kb[i + 1] : h_out;
                                 flag(T_before, ev.galpha, h.id);
                                 flag(st.T, 1.0f, nx.id);
@@ -880,22 +983,26 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                         const bool refound = h.id == prev_id && h.t == prev_t;
                         if (acc && round_start && prev_t == prev_t && !refound) {
                             const float gg = gap(h.t, prev_t);
-                            m_b = std::min(m_b, gg);
-                            if (gg < FLAG_BOUND_EPS) flag(T_before, ev.galpha, h.id);
+                            const float ge = std::max(FLAG_BOUND_EPS, CU * (h.kt + prev_kt));
+                            m_b = std::min(m_b, normMargin(gg, FLAG_BOUND_EPS, ge));
+                            if (gg < ge) flag(T_before, ev.galpha, h.id);
                         }
                         if (acc && prev_acc_t == prev_acc_t && !refound) {
                             const float gg = gap(h.t, prev_acc_t);
-                            m_t = std::min(m_t, gg);
-                            if (gg < FLAG_PAIR_EPS) {  // may swap, or tie and lose one at a round boundary
+                            const float ge = std::max(FLAG_PAIR_EPS, CU * (h.kt + prev_acc_kt));
+                            m_t = std::min(m_t, normMargin(gg, FLAG_PAIR_EPS, ge));
+                            if (gg < ge) {  // may swap, or tie and lose one at a round boundary
                                 flag(prev_acc_T, prev_acc_a, prev_id_acc);
                                 flag(T_before, ev.galpha, h.id);
                             }
                         }
                         round_start = false;
                         prev_t = h.t;
+                        prev_kt = h.kt;
                         prev_id = h.id;
                         if (acc) {
                             prev_acc_t = h.t;
+                            prev_acc_kt = h.kt;
                             prev_acc_T = T_before;
                             prev_acc_a = ev.galpha;
                             prev_id_acc = h.id;
@@ -908,10 +1015,12 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
                         if (acc && !(st.T > P->min_transmittance)) {
                             const Hit nx = i + 1 < MAX_HIT_PER_TRACE && kb[i + 1].id != INVALID_PARTICLE_ID ? kb[i + 1]
                                                                                                           : h_out;
-                            if (nx.id != INVALID_PARTICLE_ID && gap(h.t, nx.t) < 1e-4f && accepted(nx.id)) {
+                            if (nx.id != INVALID_PARTICLE_ID && gap(h.t, nx.t) < teps(FLAG_BOUND_EPS, h, nx) &&
+                                accepted(nx.id)) {
                                 const float gg = gap(h.t, nx.t);
-                                m_b = std::min(m_b, gg);
-                                if (gg < FLAG_BOUND_EPS) {
+                                const float ge = teps(FLAG_BOUND_EPS, h, nx);
+                                m_b = std::min(m_b, normMargin(gg, FLAG_BOUND_EPS, ge));
+                                if (gg < ge) {
                                     flag(T_before, ev.galpha, h.id);
                                     flag(T_before, evalResponse(s, nx.id, o, d).galpha, nx.id);
                                 }

@@ -20,7 +20,8 @@ class OracleParams(C.Structure):
                 ("sph_eval_degree", C.c_uint32), ("alpha_min", C.c_float), ("pixel_offset", C.c_float),
                 ("alpha_init", C.c_float), ("tmin_inclusive", C.c_uint32), ("proxy_mode", C.c_uint32),
                 ("drop_rejected", C.c_uint32), ("max_rounds", C.c_uint32), ("ray_dirs_layout", C.c_uint32),
-                ("kernel_min_response", C.c_float), ("kernel_opts", C.c_uint32), ("kernel_degree", C.c_float)]
+                ("kernel_min_response", C.c_float), ("kernel_opts", C.c_uint32), ("kernel_degree", C.c_float),
+                ("perturb_ulps", C.c_uint32), ("flag_cond_ulps", C.c_float)]
 
 
 _lib = None
@@ -82,6 +83,8 @@ def default_params(**kw):
     p.kernel_min_response = 0.0113
     p.kernel_opts = 0
     p.kernel_degree = 4.0
+    p.perturb_ulps = 0
+    p.flag_cond_ulps = COND_ULPS
     for k, v in kw.items():
         if k == "aabb":
             p.aabb[:] = list(v)
@@ -210,16 +213,19 @@ class Scene:
         return out[:min(n, maxn)]
 
 
-# Parity accounting (see out_margin in gvrt_oracle.cpp): a ray is "on a threshold" when one of its
-# composite decisions lies within THR_EPS (relative) of the hit / alpha / transmittance threshold, two
-# consecutive accepted crossings lie within PAIR_EPS in t, or a crossing at a round / buffer /
-# termination boundary lies within BOUND_EPS in t of its neighbour (or ties bitwise at the exclusive
-# tmin).  Only such rays may decide differently under a few-ulp different float evaluation (the GPU's
-# v_exp / v_rsq / v_rcp and FMA contraction; the t of a crossing is measured to differ by up to ~1e-6
-# relative); every other ray must match.
+# Parity accounting (see out_margin in gvrt_oracle.cpp): a ray is "on a threshold" when one of its composite
+# decisions lies within its float uncertainty of the threshold: the larger of a fixed relative epsilon -- THR_EPS for
+# the hit / alpha / transmittance thresholds, PAIR_EPS between consecutive accepted crossings in t, BOUND_EPS for a
+# crossing at a round / buffer / termination boundary against its neighbour (or a bitwise tie at the exclusive tmin)
+# -- and COND_ULPS ulps of the decision's own conditioning (a response of a particle far away in kernel units, a face
+# crossed at grazing incidence).  The C oracle stores each margin normalised to its fixed epsilon (distance x eps /
+# max(eps, uncertainty)), so the comparisons below are unchanged.  Only such rays may decide differently under a
+# few-ulp different float evaluation (the GPU's v_exp / v_rsq / v_rcp and FMA contraction); every other ray must
+# match.
 THR_EPS = 1e-4
 PAIR_EPS = 2e-6
 BOUND_EPS = 1e-5
+COND_ULPS = 6.0
 
 
 def _margin_rows(margin):
@@ -245,7 +251,7 @@ def flip_bound(margin):
 
 
 def flag_eps():
-    """The C oracle's flag thresholds (must equal THR_EPS, PAIR_EPS, BOUND_EPS)."""
-    out = np.zeros(3, np.float32)
+    """The C oracle's flag thresholds (must equal THR_EPS, PAIR_EPS, BOUND_EPS, COND_ULPS)."""
+    out = np.zeros(4, np.float32)
     lib().oracle_flag_eps(_p(out))
     return out

@@ -17,6 +17,9 @@ if "SQ_WAVE_CYCLES" in avg:
     wc = avg["SQ_WAVE_CYCLES"]
     out["frac_of_wave_cycles"] = {k: avg[k] / wc for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
                                                          "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_LDS") if k in avg}
+if "GRBM_GUI_ACTIVE" in avg and "SQ_INSTS_VALU" in avg:
+    # the bench line's roofline (bound "issue"): 2 x VALU wave-instructions / (1024 SIMDs x the dispatch's cycles)
+    out["valu_issue_frac"] = 2 * avg["SQ_INSTS_VALU"] / (1024 * out["gpu_cycles"])
 if "FETCH_SIZE" in avg:
     out["hbm_read_bytes_per_dispatch_x2_corrected"] = avg["FETCH_SIZE"] * 1024 * 2
 if "WRITE_SIZE" in avg:

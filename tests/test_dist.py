@@ -128,8 +128,12 @@ def _exchange_worker(rank, world, port, split, width, height, views, nframes, q)
     for _ in range(nframes):
         ex.step(render)
     ex.drain()
+    # the strong-scaling record's per-phase probe: one more frame, one phase at a time, marks in order
+    marks = []
+    ex.probe(render, marks.append, barrier=dist.barrier)
     if rank == 0:
-        q.put({k: v.copy() for k, v in got.items()})
+        q.put({"frames": {k: v.copy() for k, v in got.items()}, "marks": marks, "exchange_bytes": ex.exchange_bytes,
+               "padded": ex.padded_gather_bytes, "sizes": sizes, "send_shape": tuple(ex.send[0].shape)})
     dist.barrier()
     dist.destroy_process_group()
 
@@ -137,9 +141,10 @@ def _exchange_worker(rank, world, port, split, width, height, views, nframes, q)
 @pytest.mark.parametrize("world,split,width,height,views", [(2, "tiles", 100, 60, 1), (3, "tiles", 37, 29, 1),
                                                              (2, "views", 24, 16, 5), (3, "views", 16, 8, 3)])
 def test_frame_exchange_double_buffered(world, split, width, height, views):
-    """bench.py's N-rank path on CPU: dist.FrameExchange with two send buffers in flight, unequal parts padded
-    for the gather (tiles: ragged block counts; views: 5 views over 2 ranks), rank-0 assembly per frame.
-    Every frame arrives, in order, equal to the 1-rank frame."""
+    """bench.py's N-rank path on CPU: dist.FrameExchange with two send buffers in flight, unequal parts (tiles:
+    ragged block counts; views: 5 views over 2 ranks) sent point to point at their exact sizes (no padding: every
+    buffer has its own rank's part shape), rank-0 assembly per frame, then the strong-scaling record's one-frame
+    probe.  Every frame arrives, in order, equal to the 1-rank frame."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -148,13 +153,22 @@ def test_frame_exchange_double_buffered(world, split, width, height, views):
              for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=240)
+    res = q.get(timeout=240)
     for p in procs:
         p.join(timeout=240)
         assert p.exitcode == 0
-    assert sorted(got) == list(range(nframes))
-    for k in range(nframes):
+    got = res["frames"]
+    assert sorted(got) == list(range(nframes + 1))
+    for k in range(nframes + 1):
         np.testing.assert_array_equal(got[k], frame_pattern(k, width, height, views))
+    assert res["marks"] == ["rendered", "posted", "exchanged", "assembled"]
+    sizes = res["sizes"]
+    item = 4 if split == "tiles" else height * width * 4
+    assert res["send_shape"][0] == sizes[0]
+    assert res["exchange_bytes"] == sum(sizes[1:]) * item  # exact parts: no padding on the wire
+    assert res["padded"] == (world - 1) * max(sizes) * item
+    if len(set(sizes)) > 1:
+        assert res["exchange_bytes"] < res["padded"]
 
 
 def test_launch_ranks_gives_n_processes():

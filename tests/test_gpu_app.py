@@ -69,6 +69,10 @@ def test_bench_on_a_ply(gv, tmp_path):
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["data"] == "real scene scene.ply" and line["config"]["gaussians"] == 5000
     assert line["value"] > 0 and line["roofline"]["frac"] > 0
+    # the roofline names its binding unit (instruction issue, from the PMC passes) and is a bound
+    roof = line["roofline"]
+    assert roof["bound"] == "issue" and roof["frac"] <= 1.0, roof
+    assert 0.0 < roof["hbm"]["frac"] < 1.0 and roof["logical"]["bound"] == "hbm"
 
 
 def test_cpp_app_flows_match_python(gv, tmp_path):
@@ -139,3 +143,43 @@ def test_cpp_rccl_split_frame_one_rank(gv, tmp_path, layout):
         import json
         d = json.loads(line)
         assert d["identical_to_one_gpu"] is True and d["world"] == 1 and d["ms_per_frame"] > 0
+
+
+def _split(exe, ply, tmp_path, tag, *extra, timeout=180):
+    import subprocess
+    return subprocess.run([exe, "split", "--ply", ply, "--rank", "0", "--world", "1", "--id-file",
+                           str(tmp_path / f"rccl_{tag}.id"), "--out", str(tmp_path / f"split_{tag}"), *extra],
+                          capture_output=True, text=True, timeout=timeout,
+                          env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+
+
+def test_cpp_rccl_split_views_one_rank(gv, tmp_path):
+    """Config 5 through the native C++ path: SplitFrame::VIEWS over a 16-view light-field rig --
+    rank 0 times each view alone, one ncclBroadcast of the costs (with its status word), balanced_views, this rank's
+    views in one batched launch, each view sent whole into its slot of the rig frame -- with a one-rank
+    communicator: the gathered 16 views equal one batched render of the rig on this GPU byte for byte."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "3dgvrt_lightfield_amd", "gvrt_app")
+    ply = str(tmp_path / "scene.ply")
+    gv.save_ply(ply, gv.scene.config1(n=3000))
+    import json
+    r = _split(exe, ply, tmp_path, "views", "--frames", "3", "--width", "96", "--height", "64", "--layout", "views",
+               "--views", "16")
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["identical_to_one_gpu"] is True and d["views"] == 16 and d["assignment"] == [list(range(16))]
+
+
+def test_cpp_rccl_split_calibration_failure_is_a_status(gv, tmp_path):
+    """a failed tile-cost calibration on rank 0 (here injected: the handle's tile_order is off, so
+    gvrt_read_tile_costs has no costs to read) travels with the status word of the one broadcast every rank enters:
+    SplitFrame reports it as a status and the app exits with it, promptly, instead of leaving peers in a
+    collective."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "3dgvrt_lightfield_amd", "gvrt_app")
+    ply = str(tmp_path / "scene.ply")
+    gv.save_ply(ply, gv.scene.config1(n=2000))
+    r = _split(exe, ply, tmp_path, "fail", "--frames", "2", "--width", "64", "--height", "64", "--layout",
+               "cost-bands", "--tile-order-off", timeout=120)
+    assert r.returncode == 1, (r.returncode, r.stdout[-500:], r.stderr[-1000:])
+    assert "tile-cost calibration failed on rank 0" in r.stderr and "gvrt_read_tile_costs" in r.stderr

@@ -37,11 +37,22 @@ def _bench(args, distributed):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("split", ["views", "tiles"])
-def test_bench_exchange_step_matches_single_gpu(split):
+@pytest.mark.parametrize("split,strong", [("views", "bicycle"), ("tiles", "bicycle,truck")])
+def test_bench_exchange_step_matches_single_gpu(split, strong):
+    """Also the N-rank line's strong-scaling sub-records: the bicycle 1080p frame (and the truck 4K
+    frame) tile-split in cost bands through the exact-size exchange, per-rank kernel / exchange / assembly times,
+    the exchanged bytes, and the assembled frame equal to rank 0's one-GPU frame."""
     args = ["--config", "bicycle", "--split", split]
-    one = _bench(args, distributed=False)
-    ex = _bench(args, distributed=True)
+    one = _bench(args + ["--strong", "none"], distributed=False)
+    ex = _bench(args + ["--strong", strong], distributed=True)
     assert one["frame_sha1"] and ex["frame_sha1"] == one["frame_sha1"], (ex["frame_sha1"], one["frame_sha1"])
     assert ex["n_gpus"] == 1 and ex["config"]["split"] == split
     assert ex["value"] > 0 and ex["ms_per_step"] > 0
+    recs = ex["strong_scaling"]
+    assert [r["frame"].split()[0] for r in recs] == strong.split(",")
+    for r in recs:
+        assert r["identical_to_one_gpu"] is True, r
+        assert r["ranks"] == 1 and r["layout"] == "cost-bands" and r["ms_per_frame"] > 0 and r["mrays"] > 0
+        assert len(r["kernel_ms_per_rank"]) == len(r["exchange_ms_per_rank"]) == 1 and r["kernel_ms_per_rank"][0] > 0
+        assert r["exchange_bytes"] == 0 and r["bytes_sent_per_rank"][0] == r["tiles_per_rank"][0] * 256
+        assert r["one_gpu_kernel_ms"] > 0 and r["assemble_ms"] >= 0

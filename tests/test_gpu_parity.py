@@ -4,16 +4,19 @@ Tolerances (north star: "pixel-for-pixel within a stated float tolerance", PSNR 
   * enclosing records: rtol 2e-6 / atol 1e-7 (expf / 1/sqrt ulps; FMA contraction on gfx950)
   * survivor count and compaction order: exact
   * render, float RGBA vs the oracle with the same analytic proxy, every compared ray:
-      - rays "on a threshold" (oracle.ambiguous): one of the ray's composite decisions came within a relative
-        1e-4 of a threshold (response vs hitMinGaussianResponse, alpha vs 1/255, T vs minTransmittance), two
-        consecutive composited crossings within 2e-6 in t, or a crossing at a round / full-buffer / termination
-        boundary within 1e-5 of its neighbour (or a bitwise tie dropped at the exclusive tmin, Q13).  Only these
-        rays may decide differently under the GPU's few-ulp exp / rsqrt / rcp.  Their fraction is capped per
-        configuration (default 2 %), and each of them is still bounded: |d rgb| <= the oracle's flip bound
-        (oracle.flip_bound: per flagged decision T x alpha moved x the largest radiance channel on the ray,
-        plus minTransmittance x that channel) + 1e-4;
-      - every other ray: |d rgb| <= 1e-4 on >= 99.99 % of them, max |d rgb| <= 5e-3, and the accepted-hit
-        count (alpha channel) equal;
+      - rays "on a threshold" (oracle.ambiguous): one of the ray's composite decisions lies within its float
+        uncertainty of a threshold -- the larger of a fixed relative epsilon (1e-4 for the response vs
+        hitMinGaussianResponse, alpha vs 1/255 and T vs minTransmittance; 2e-6 between consecutive composited
+        crossings; 1e-5 at a round / full-buffer / termination boundary) and 6 ulps of the decision's own conditioning
+        (the response of a particle far away in kernel units, a face crossed at grazing incidence: gvrt_oracle.cpp
+        FLAG_COND_ULPS) -- or a bitwise tie dropped at the exclusive tmin (Q13).  Only these rays may decide
+        differently under the GPU's few-ulp exp / rsqrt / rcp and FMA order.  Their fraction is capped per
+        configuration near its measured value, and each of them is still bounded: |d rgb| <= the oracle's flip bound
+        (oracle.flip_bound: per flagged decision T x alpha moved x the largest radiance channel on the ray, plus
+        minTransmittance x that channel) + 1e-4;
+      - every other ray: |d rgb| <= 1e-4 and the accepted-hit count (alpha channel) equal, with no exception
+        (frac_tol 0; round 3 allowed 1e-4 of them beyond, up to 5e-3: each of those was an ill-conditioned threshold or
+        pair decision, now flagged, DESIGN.md §5);
       - all compared rays together: rgba8 PSNR >= 50 dB.
   * render vs the literal restatement (20-triangle soup, watertight triangle test): PSNR >= 50 dB
 """
@@ -28,7 +31,7 @@ RTOL, ATOL = 2e-6, 1e-7
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def _cmp_images(a, ref, margin=None, frac_tol=1e-4, tol=1e-4, max_tol=5e-3, amb_max=0.02, psnr_min=50.0):
+def _cmp_images(a, ref, margin=None, frac_tol=0.0, tol=1e-4, max_tol=1e-4, amb_max=0.02, psnr_min=50.0):
     """a: HIP rgba; ref: oracle output dict (rgba32f + margin) or a bare rgba array with `margin` given.
     See the module docstring for the accounting; returns the number of on-threshold rays."""
     if isinstance(ref, dict):
@@ -519,8 +522,8 @@ def test_bicycle_full_frame_vs_oracle_and_fast_literal(gv, O, bicycle):
         ref = sc.render(vi, pi, W, H, margin=True)
     finally:
         sc.close()
-    _cmp_images(fast["rgba32f"], ref, amb_max=0.015)
-    _cmp_images(lit["rgba32f"], ref, amb_max=0.015)
+    _cmp_images(fast["rgba32f"], ref, amb_max=0.02)  # 1.48 % flagged (conditioning-aware flags)
+    _cmp_images(lit["rgba32f"], ref, amb_max=0.02)
     record_parity("bicycle", **parity_figures(O, gv, fast["rgba32f"], ref), fast_literal_differ=n)
 
 
@@ -580,6 +583,71 @@ def test_accept_boxes_follow_the_thresholds(gv):
     for a, b in zip(frames[1], frames[0]):
         np.testing.assert_array_equal(a, b)
     assert not np.array_equal(frames[1][0], frames[1][2])  # the thresholds do change the image
+
+
+@pytest.mark.parametrize("case", ["adaptive_0.0113", "adaptive_0.05", "rig_2x2"])
+def test_accept_boxes_other_kernels_bit_identical(gv, case):
+    """the two other kernels that read the acceptance-box nodes -- the ADAPTIVE packed kernel (enclosing
+    opts = 1: the proxy's kernel scale, hence D in k_accept_leaf, follows each particle's density) and the multi-origin
+    OKCAM kernel of a light-field rig -- give the frame of the proxy-box nodes bit for bit, for several thresholds."""
+    s = gv.scene.dense_standin(60_000, seed=5)
+    W, H = 160, 96
+    enc = {}
+    if case.startswith("adaptive"):
+        enc = dict(opts=1, kernel_min_response=float(case.split("_")[1]))
+        vi, pi = gv.scene.mipnerf_camera(W, H)
+        ncams = 1
+    else:
+        vi, pi = gv.camera.lightfield_grid_rig(gv.camera.orbit_eye(4.0, 20.0, 60.0), (0.0, 0.0, 0.0), nx=2, ny=2,
+                                               spacing=0.1, aspect=gv.camera.aspect_ratio(W, H))
+        ncams = 4
+    cases = [{}, dict(alpha_min=0.05), dict(hit_min_gaussian_response=0.004), {}]
+    frames = {}
+    for opt in (1, 0):
+        with gv.Renderer(0) as r:
+            r.set_option("accept_boxes", opt)
+            r.prepare(s, builder=2, collapse=1, **enc)
+            frames[opt] = [r.render(vi, pi, W, H, ncams=ncams, **kw)["rgba32f"] for kw in cases]
+    for a, b in zip(frames[1], frames[0]):
+        np.testing.assert_array_equal(a, b)
+    assert (frames[1][0][..., 3] > 0).mean() > 0.3  # the scene covers the frames
+
+
+def test_optional_copies_that_do_not_fit_change_no_pixel(gv, config1):
+    """the record-origin copies (single origin: two copies; a rig: one per camera), like the octant and
+    acceptance node copies, are an optional speed-up.  When one does not fit -- forced here by the handle's
+    optional_mem_mb budget, the path a failing hipMalloc takes -- the launch runs without it: no error, and the frame
+    of the default handle bit for bit, for a single camera and a 2x2 rig, at a budget below everything and at one
+    that leaves room for the node copies but not for every record copy."""
+    W = H = 96
+    vi, pi = gv.scene.config1_camera(W, H)
+    rvi, rpi = gv.camera.lightfield_grid_rig(gv.camera.orbit_eye(3.9, 10.0, 0.0), (0.0, 0.0, 0.0), nx=2, ny=2,
+                                             spacing=0.2, aspect=1.0)
+
+    def frames(budget_mb=0, record_origins=1):
+        with gv.Renderer(0) as r:
+            r.set_option("optional_mem_mb", budget_mb)  # before prepare: the octant copies are made by the build
+            r.set_option("record_origins", record_origins)
+            r.prepare(config1)
+            a = r.render(vi, pi, W, H)["rgba32f"]
+            b = r.render(rvi, rpi, W, H, ncams=4)["rgba32f"]
+            a2 = r.render(vi, pi, W, H)["rgba32f"]
+            return a, b, a2, int(r.stats()["device_bytes"])
+
+    a0, b0, _, full = frames()
+    a1, b1, _, no_rec = frames(record_origins=0)
+    assert full > no_rec  # the default handle holds the record copies
+    for budget in (1, (no_rec >> 20) + 1):
+        a, b, a2, used = frames(budget_mb=budget)
+        np.testing.assert_array_equal(a, a0)
+        np.testing.assert_array_equal(a2, a0)
+        np.testing.assert_array_equal(b, b0)
+        assert used < full
+    np.testing.assert_array_equal(a1, a0)
+    np.testing.assert_array_equal(b1, b0)
+    with gv.Renderer(0) as r:
+        with pytest.raises(gv.GvrtError):
+            r.set_option("optional_mem_mb", -1)
 
 
 def test_read_tile_costs(gv, config1):

@@ -225,3 +225,19 @@ def test_cpp_cost_bands_match_python(gv, tmp_path, W, H, world):
                   "--layout", "bands", "--costs", str(f))
         got = np.array([[int(v) for v in l.split()] for l in out.splitlines()], np.int64).reshape(-1, 3)
         np.testing.assert_array_equal(got, ref[rank].astype(np.int64)[:, :3])
+
+
+@pytest.mark.parametrize("views,world,seed", [(16, 8, 0), (16, 3, 1), (16, 16, 2), (7, 2, 3), (5, 8, 4), (16, 5, 5)])
+def test_cpp_balanced_views_match_python(views, world, seed):
+    """The C++ host's view split (gvrt_rccl.h balanced_views, SplitFrame::VIEWS: config 5 on N GPUs) assigns the same
+    views to the same ranks as the Python layer (dist.balanced_views) from the same per-view costs, ties included
+    (costs drawn from a few values, so equal costs occur), and every view once."""
+    import importlib
+    dist = importlib.import_module("3dgvrt_lightfield_amd.dist")
+    rng = np.random.default_rng(seed)
+    costs = rng.choice([0.72, 0.9, 1.1, 1.25, 1.4], size=views) * rng.choice([1.0, 1.0, 1.003], size=views)
+    out = run("views", "--costs", ",".join(repr(float(c)) for c in costs), "--world", str(world))
+    lines = out.splitlines()
+    got = [[int(v) for v in l.split()] for l in lines] + [[] for _ in range(world - len(lines))]
+    assert got == dist.balanced_views(costs.tolist(), world)
+    assert sorted(v for g in got for v in g) == list(range(views))

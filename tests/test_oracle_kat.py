@@ -238,7 +238,7 @@ def test_camera_math(gv):
 
 
 def test_flag_thresholds_shared_with_the_c_oracle(O):
-    np.testing.assert_array_equal(O.flag_eps(), np.array([O.THR_EPS, O.PAIR_EPS, O.BOUND_EPS], np.float32))
+    np.testing.assert_array_equal(O.flag_eps(), np.array([O.THR_EPS, O.PAIR_EPS, O.BOUND_EPS, O.COND_ULPS], np.float32))
 
 
 @pytest.mark.parametrize("kw", [{k: v * (1 + sgn * 9e-5)} for k, v in (("hit_min_gaussian_response", 0.0113),
@@ -261,3 +261,61 @@ def test_flip_bound_covers_threshold_perturbations(gv, O, config1, config1_enc, 
     assert amb[changed].all()                  # only on flagged rays
     assert (d[changed] <= fb[changed] + 1e-6).all(), (d[changed] / fb[changed]).max()
     assert (fb[~amb] == 0).all() and (fb[amb] > 0).mean() > 0.5
+
+
+@pytest.fixture(scope="module")
+def mipnerf_small(gv, O):
+    """A 200 k-Gaussian config-2 stand-in (small particles seen from afar: the ill-conditioned responses of VERDICT
+    r03's unflagged outliers) and its oracle scene."""
+    s = gv.scene.mipnerf_standin(200_000, 1)
+    e = O.enclose(s)
+    sc = O.Scene(e)
+    yield sc
+    sc.close()
+
+
+@pytest.mark.parametrize("ulps", [1, 2, 4])
+def test_conditioning_flags_cover_another_float_evaluation(gv, O, mipnerf_small, ulps):
+    """the unflagged rays that differed from the GPU by more than 1e-4 (bicycle 6, light field 2, dense
+    1; scripts/parity_outliers.py) were a particle's pair of crossings whose response lay 1.05-1.45e-4 from
+    hitMinGaussianResponse with a relative float uncertainty of the same size (|gro| of 200-400: the line's distance
+    from the centre is a difference of products ~|gro|), and, on the dense scene, two composited crossings 6.8e-6 apart
+    in t while a face crossed at grazing incidence makes t uncertain by more.  The oracle now flags a decision within
+    FLAG_COND_ULPS (6) ulps of its own conditioning, whichever is larger than the fixed epsilon.
+
+    Checked here by "another float evaluation": the same frame with the ray direction and every particle's kernel-frame
+    origin and direction moved by up to `ulps` ulps (perturb_ulps; the GPU's ray direction differs from the oracle's
+    by 0-3 ulps per component, measured).  Every accept decision that moves is on a flagged ray, every ray that moves
+    by more than 1e-4 is flagged (at 4 ulps: up to 2 e-4 of alpha drift without a moved decision) and within its flip
+    bound."""
+    W, H = 480, 270
+    vi, pi = gv.scene.mipnerf_camera(W, H)
+    a = mipnerf_small.render(vi, pi, W, H, margin=True)
+    b = mipnerf_small.render(vi, pi, W, H, perturb_ulps=ulps)
+    amb = O.ambiguous(a["margin"])
+    fb = O.flip_bound(a["margin"])
+    assert 0.003 < amb.mean() < 0.015, amb.mean()
+    d = np.abs(a["rgba32f"][:, :3] - b["rgba32f"][:, :3]).max(axis=1)
+    moved = a["stats"][:, 1] != b["stats"][:, 1]
+    assert moved.sum() > 0 and not (moved & ~amb).any()  # decisions move, only on flagged rays
+    assert (d[amb] <= fb[amb] + 1e-4).all()
+    tol = 1e-4 if ulps <= 2 else 2e-4
+    assert d[~amb].max() <= tol, d[~amb].max()
+
+
+def test_conditioning_flags_catch_the_r03_outlier_class(gv, O, mipnerf_small):
+    """Without the conditioning term (flag_cond_ulps 0: the fixed 1e-4 / 2e-6 / 1e-5 margins of round 3) the same
+    perturbation moves accept decisions on unflagged rays, and unflagged rays by more than 1e-4: the class exists in
+    this scene, and the conditioning term is what covers it (at about twice the flagged fraction)."""
+    W, H = 480, 270
+    vi, pi = gv.scene.mipnerf_camera(W, H)
+    a0 = mipnerf_small.render(vi, pi, W, H, margin=True, flag_cond_ulps=0.0)
+    a = mipnerf_small.render(vi, pi, W, H, margin=True)
+    np.testing.assert_array_equal(a0["rgba32f"], a["rgba32f"])  # the margins are accounting only
+    b = mipnerf_small.render(vi, pi, W, H, perturb_ulps=2)
+    amb0, amb = O.ambiguous(a0["margin"]), O.ambiguous(a["margin"])
+    assert (amb0 <= amb).all() and amb.mean() < 3 * amb0.mean()
+    d = np.abs(a["rgba32f"][:, :3] - b["rgba32f"][:, :3]).max(axis=1)
+    moved = a["stats"][:, 1] != b["stats"][:, 1]
+    assert (moved & ~amb0).sum() >= 3 and ((d > 1e-4) & ~amb0).sum() >= 3
+    assert not (moved & ~amb).any() and not ((d > 1e-4) & ~amb).any()
