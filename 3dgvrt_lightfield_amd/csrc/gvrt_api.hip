@@ -265,6 +265,9 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
     c->okrecs_valid[0] = c->okrecs_valid[1] = false;
     c->recs_cams_ok = false;
     c->okrecs_nomem = c->recs_cams_nomem = false;
+    c->leaf_hk_ok = false;
+    gvrt_dfree(c, (void**)&c->d_leaf_hk);
+    c->wide_ok = false;
     gvrt_dfree(c, (void**)&c->d_nodes4x8);
     gvrt_dfree(c, (void**)&c->d_nodes4e);
     gvrt_dfree(c, (void**)&c->d_nodes4ex8);
@@ -674,6 +677,15 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
                       std::ldexp(omax, -20) <= c->box_pad_abs;  // also false for a NaN origin
     }
     a.kfast = p->kbuffer_depth ? p->kbuffer_depth : (uint32_t)K_FAST_DEFAULT;
+    // adaptive enclosing: the per-leaf icosahedron half-widths, once per build
+    if ((c->enc.opts & 1u) && c->n_leaves) {
+        if (!c->leaf_hk_ok) {
+            if (!c->d_leaf_hk && (s = gvrt_dalloc(c, (void**)&c->d_leaf_hk, 4 * c->n_leaves))) return s;
+            if ((s = gvrt_launch_leaf_hk(c))) return s;
+            c->leaf_hk_ok = true;
+        }
+        a.leaf_hk = c->d_leaf_hk;
+    }
     // FAST launches traverse the acceptance-box nodes (gvrt_launch_accept_nodes), refit when the acceptance
     // thresholds change; LITERAL launches keep every crossing and so the proxy boxes
     if (p->mode == GVRT_MODE_FAST && c->opt[GVRT_OPT_ACCEPT_BOXES] && !c->split_cells &&
@@ -684,6 +696,22 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         if (c->accept_ok) {
             a.nodes = c->d_nodes4e;
             a.nodes8 = c->opt[GVRT_OPT_OCTANT_NODES] ? c->d_nodes4ex8 : nullptr;
+        }
+    }
+    // Tile-beam traversal of the 64-wide node copies (option GVRT_OPT_WIDE_NODES): FAST launches at the default depth,
+    // built on first use after a build (and when the acceptance thresholds change); a copy that does not fit, or a
+    // tree deeper than the kernel's level buffers, leaves the launch on the packet traversal
+    if (c->opt[GVRT_OPT_WIDE_NODES] && p->mode == GVRT_MODE_FAST && a.kfast == (uint32_t)K_FAST_DEFAULT &&
+        !(c->enc.opts & 1u) && a.nrecs < 0xFFFFFFu && c->opt[GVRT_OPT_PACKED_KBUFFER] && !c->split_cells) {
+        const bool acc = c->opt[GVRT_OPT_ACCEPT_BOXES] && (p->hit_min_gaussian_response > 0.0f || p->alpha_min > 0.0f);
+        if (!c->wide_ok || c->wide_accept != acc ||
+            (acc && (c->wide_key[0] != p->hit_min_gaussian_response || c->wide_key[1] != p->alpha_min))) {
+            GVRT_HIP(c, hipStreamSynchronize(c->stream));  // queued launches may read the copies being replaced
+            if ((s = gvrt_build_wide(c, acc, p->hit_min_gaussian_response, p->alpha_min))) return s;
+        }
+        if (c->wide_ok) {
+            a.wide = c->d_wide;
+            a.wide_stride = c->n_wide * WIDE_W;
         }
     }
     // Single-origin FAST launches at the default depth read each leaf's kernel-frame origin ok from its record:

@@ -348,6 +348,18 @@ __device__ inline RenderRec load_rec_at(const RenderRec* __restrict__ base, int3
     asm volatile("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
     return __builtin_bit_cast(RenderRec, v);
 }
+// ADAPTIVE: the record and its leaf's icosahedron half-width (k_leaf_hk) in one round trip
+__device__ inline RenderRec load_rec_hk_at(const RenderRec* __restrict__ base, const float* __restrict__ hkbase,
+                                           int32_t idx, float& hk) {
+    sv16 v;
+    float h;
+    const uint32_t off = (uint32_t)idx << 6, off4 = (uint32_t)idx << 2;
+    asm volatile("s_load_dwordx16 %0, %2, %4\n\ts_load_dword %1, %3, %5\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(v), "=&s"(h)
+                 : "s"(base), "s"(hkbase), "s"(off), "s"(off4));
+    hk = h;
+    return __builtin_bit_cast(RenderRec, v);
+}
 #define NODE_BOX(nd, k, j) (nd).f(6 * (k) + (j))
 #define NODE_CHILD(nd, k) (nd).w(24 + (k))
 #define NODE_PAD(nd, j) (nd).w(29 + (j))
@@ -376,6 +388,23 @@ __device__ inline int launder_lane(int l) {
     return l;
 }
 __device__ inline uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+// Wave-wide min / max of a float by DPP (quad permutes, row half-mirror and mirror, then the row broadcasts of
+// GFX9), the result in lane 63 (all 64 lanes take part; callers pass a neutral value for lanes that should not count)
+template <int CTRL, int ROWMASK>
+__device__ inline float dppf(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, ROWMASK, 0xf, false));
+}
+__device__ inline float wave_maxf(float v) {
+    v = fmaxf(v, dppf<0xB1, 0xf>(v));   // quad_perm [1,0,3,2]
+    v = fmaxf(v, dppf<0x4E, 0xf>(v));   // quad_perm [2,3,0,1]
+    v = fmaxf(v, dppf<0x141, 0xf>(v));  // row_half_mirror
+    v = fmaxf(v, dppf<0x140, 0xf>(v));  // row_mirror
+    v = fmaxf(v, dppf<0x142, 0xa>(v));  // row_bcast:15
+    v = fmaxf(v, dppf<0x143, 0xc>(v));  // row_bcast:31
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ inline float wave_minf(float v) { return -wave_maxf(-v); }
 __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Dispatch geometry.  One wave per workgroup: a finished wave's slot and LDS go to the next tile at once
@@ -383,10 +412,102 @@ __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlan
 // list, workgroups walk ST_W x ST_H supertiles of tiles in row-major order (0.9 / 2.0 / 1.8 % faster than
 // row-major tiles).  4 waves per SIMD (<= 128 VGPRs) measured fastest, ahead of 3 (no spills) and 5 (heavy
 // spills or a smaller k-buffer).
+// One leaf (record li) for the lanes in bk: response, icosahedron clip, k-buffer insertion.  A macro, expanded by the
+// packet and the wide traversal, so that each keeps its own inlined copy (as a lambda capturing the k-buffer by
+// reference the packet kernel spilled 8 B per lane).
+#define GVRT_LEAF(LI_, BK_)                                                                                        \
+    {                                                                                                              \
+        const int32_t li = (LI_);                                                                                  \
+        const uint64_t bk = (BK_);                                                                                 \
+        float hk_leaf = 0.0f;                                                                                      \
+        const RenderRec rec =                                                                                      \
+            ADAPTIVE ? load_rec_hk_at(recw, a.leaf_hk, unii(li), hk_leaf) : load_rec_at(recw, unii(li));           \
+        if constexpr (ADAPTIVE) hk_leaf = to_vgpr(hk_leaf);                                                        \
+        /* split (SplitBLAS analogue): the piece's proxy id and cell; cell == ~0u admits every crossing */         \
+        uint4 pa = make_uint4((uint32_t)li, 0xFFFFFFFFu, 0u, 0u);                                                  \
+        if (aux_) pa = aux_[li];                                                                                   \
+        {                                                                                                          \
+            const uint32_t gi = uni(pa.x);                                                                         \
+            wadd(W_LEAVES, 1);                                                                                     \
+            if (__builtin_amdgcn_inverse_ballot_w64(bk)) {  /* exec &= bk: no per-lane bit test */                 \
+                ladd(L_LEAVES);                                                                                    \
+                /* ---- leaf: response (processHit's math) + analytic icosahedron clip */                          \
+                f3 ok, dk;                                                                                         \
+                kernel_frame<OKREC, true>(rec, o, d, ok, dk);                                                      \
+                /* Conservative pre-reject: gres > hitMinGaussianResponse needs the squared line */                \
+                /* distance gd = |dk x ok|^2 / |dk|^2 below sqrt(ln(minResponse)/S) (a.gpre carries a */           \
+                /* 1e-3 margin), so most proxies are rejected without the sqrt / exp below. */                     \
+                const float l2 = len2(dk);                                                                         \
+                const f3 cu = cross3(dk, ok);                                                                      \
+                const bool maybe = (cu.x * cu.x + cu.y * cu.y + cu.z * cu.z) < a.gpre * l2;                        \
+                bool acc = false;                                                                                  \
+                float galpha = 0.0f;                                                                               \
+                if (maybe) acc = particle_alpha(ok, dk, l2, rec.density, a.min_response, a.alpha_min, galpha);     \
+                if (LITERAL || acc) {                                                                              \
+                    /* (adaptive: sqrt(3) kernelScale(density) of the leaf, precomputed by k_leaf_hk with the */   \
+                    /* same kernel_scale arithmetic) */                                                            \
+                    const float hk = ADAPTIVE ? hk_leaf : a.kernel_h;                                              \
+                    float tn, tf;                                                                                  \
+                    ico_clip(ok, dk, hk, tn, tf);                                                                  \
+                    if (tn <= tf) {                                                                                \
+                        const float al = acc ? galpha : -1.0f;                                                     \
+                        /* (an inclusive tmin exists only in LITERAL mode: the API refuses it otherwise) */        \
+                        const bool incl = LITERAL && a.tmin_inclusive;                                             \
+                        bool in0 = (incl ? tn >= tlo : tn > tlo) && tn <= thi;                                     \
+                        bool in1 = (incl ? tf >= tlo : tf > tlo) && tf <= thi;                                     \
+                        if (uni(pa.y) != 0xFFFFFFFFu) {                                                            \
+                            in0 = in0 && crossing_cell(o, d, tn, a, pa.z, pa.w) == pa.y;                           \
+                            in1 = in1 && crossing_cell(o, d, tf, a, pa.z, pa.w) == pa.y;                           \
+                        }                                                                                          \
+                        const float ta = in0 && tn < tcut ? tn : (in1 && tf < tcut ? tf : INF_DIST);               \
+                        const float tb = (in0 && in1 && tf < tcut) ? tf : INF_DIST;                                \
+                        if (ta < kt[KB - 1]) {                                                                     \
+                          if constexpr (PACK) {                                                                    \
+                            const uint32_t q = alpha_code(galpha);                                                 \
+                            kb_insert2p<KB>(ta, tb, (gi << 8) | q, kt, kid);                                       \
+                            /* termination cull on the q codes (see kb_insert2p): the first slot */                \
+                            /* whose running sum reaches qneed is the last one composited; no */                   \
+                            /* slot can reach it while the inserted total is still below */                        \
+                            qtot += tb < INF_DIST ? 2 * q : q;                                                     \
+                            if (__builtin_amdgcn_ballot_w64(qtot >= qneed)) {                                      \
+                            uint32_t qs = 0;                                                                       \
+                            float tt = INF_DIST;                                                                   \
+_Pragma("unroll")                                                                                                  \
+                            for (int i = 0; i < KB; ++i) {                                                         \
+                                qs += kid[i] & 0xFFu;                                                              \
+                                tt = fminf(tt, qs >= qneed ? kt[i] : INF_DIST);                                    \
+                            }                                                                                      \
+                            tcut = fminf(tcut, tt);                                                                \
+                            }                                                                                      \
+                          } else {                                                                                 \
+                            kb_insert2<KB>(ta, tb, gi, al, kt, kid, ka);                                           \
+                            /* Termination-aware cull distance: walking the sorted slots with the */               \
+                            /* composite's T update, the first slot after which T <= minTransmittance */           \
+                            /* is the last one that can ever be composited (the loop ends there), so */            \
+                            /* nothing farther is needed.  The 1e-4 margin keeps the bound */                      \
+                            /* conservative against ulp differences from the composite's arithmetic. */            \
+                            float Tp = s_T[LL], tt = INF_DIST;                                                     \
+                            const float term_cut = a.min_transmittance * 0.9999f;                                  \
+                _Pragma("unroll")                                                                                  \
+                            for (int i = 0; i < KB; ++i) {                                                         \
+                                const bool acc_i = kid[i] != INVALID_ID && ka[i] > 0.0f;                           \
+                                Tp = acc_i ? Tp * (1.0f - ka[i]) : Tp;                                             \
+                                tt = (tt == INF_DIST && acc_i && Tp < term_cut) ? kt[i] : tt;                      \
+                            }                                                                                      \
+                            tcut = fminf(tcut, tt);                                                                \
+                          }                                                                                        \
+                        }                                                                                          \
+                    }                                                                                              \
+                }                                                                                                  \
+            }                                                                                                      \
+        }                                                                                                          \
+    }
+
 constexpr uint32_t ST_W = 8, ST_H = 4;
 constexpr int RENDER_MIN_WAVES = 4;
 
-template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK, bool SLACK, bool OKREC, bool OKCAM = false>
+template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK, bool SLACK, bool OKREC, bool OKCAM = false,
+          bool WIDE = false>
 __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArgs a, const Bvh4Node* __restrict__ nodes_,
                                                                  const RenderRec* __restrict__ recs_,
                                                                  const RenderRec* __restrict__ crecs_,
@@ -410,7 +531,18 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
     __shared__ float s_tmax[64];
     __shared__ uint32_t s_pxy[64];  // px | py << 16, parked for the output stage (not live in VGPRs)
     __shared__ unsigned long long s_t0;  // wave start (s_memtime), for the per-tile cost class
-    __shared__ int32_t s_stack[STACK_DEPTH];
+    __shared__ int32_t s_stack[WIDE ? 1 : STACK_DEPTH];
+    // WIDE: per level of the wide tree, the links of the visited node's 64 children (lane order = visiting order) and
+    // the mask of its hit children still to be walked
+    __shared__ int32_t s_wlink[WIDE ? WIDE_LEVELS : 1][64];
+    __shared__ unsigned long long s_wmask[WIDE ? WIDE_LEVELS : 1];
+    // STATS: the counters live in LDS, not registers (kept in registers they spilled 76-80 B per lane, so the
+    // diagnostic build had another register allocation than the shipped kernel): per wave [node visits, leaf visits,
+    // node / leaf / composite cycles, dead node visits, rounds, node visits after round 1], per lane [processed
+    // crossings, rounds, leaf tests]; every lane of the wave writes the same value to a wave counter
+    __shared__ unsigned long long s_wst[STATS ? 8 : 1];
+    __shared__ unsigned long long s_tph[STATS ? 3 : 1];  // STATS: s_memtime at the start of the node / leaf phase, wave
+    __shared__ uint32_t s_lst[STATS ? 3 : 1][64];
     // lane from mbcnt (no register input)
     const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 #define LL (PACK ? launder_lane(lane) : lane)  // FAST kernels only: LITERAL spilled more with it
@@ -487,15 +619,26 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
     s_T[lane] = 1.0f;
     s_pxy[lane] = px | py << 16;
     if (a.tile_bucket) s_t0 = __builtin_amdgcn_s_memtime();
-    // counters: only the STATS instantiation keeps them (registers); the accepted-hit count is
-    // recovered exactly from the alpha accumulator (RQ/RT alpha = alpha_init + #accepted, Q10)
-    uint32_t nproc = 0, rounds = 0;
-    uint32_t w_nodes = 0, w_leaves = 0, l_leaves = 0;  // wave node visits, wave leaf visits, lane leaf tests
-    // STATS phase timers (s_memtime, wave-uniform): node visits, leaves + insertion, composite
-    uint64_t cyc_node = 0, cyc_leaf = 0, cyc_comp = 0;
-    uint32_t w_dead = 0;  // node visits where no lane hits any child box
-    uint32_t w_rounds = 0, w_late = 0;  // traversal rounds of this wave; node visits after the first round
-    [[maybe_unused]] const uint64_t cyc_start = STATS ? __builtin_amdgcn_s_memtime() : 0;
+    // counters: the STATS instantiation keeps them in LDS (s_wst, s_lst); LITERAL keeps its round count (max_rounds)
+    // in a register.  The accepted-hit count is recovered exactly from the alpha accumulator (RQ/RT alpha =
+    // alpha_init + #accepted, Q10)
+    uint32_t rounds = 0;
+    enum { W_NODES, W_LEAVES, C_NODE, C_LEAF, C_COMP, W_DEAD, W_ROUNDS, W_LATE };
+    enum { L_NPROC, L_ROUNDS, L_LEAVES };
+    auto wadd = [&](int k, unsigned long long x) {  // wave counter += x (every lane writes the same sum)
+        if constexpr (STATS) s_wst[k] = s_wst[k] + x;
+    };
+    auto ladd = [&](int k) {  // this lane's counter += 1
+        if constexpr (STATS) {
+            const int l = lane_now();
+            s_lst[k][l] = s_lst[k][l] + 1u;
+        }
+    };
+    if constexpr (STATS) {
+        if (lane < 8) s_wst[lane] = 0ull;
+        s_lst[0][lane] = s_lst[1][lane] = s_lst[2][lane] = 0u;
+    }
+    if constexpr (STATS) s_tph[2] = __builtin_amdgcn_s_memtime();
     bool active = valid && a.nrecs > 0 && (fmaxf(0.0f, tminb - EPS_T) <= tmaxb) && (1.0f > a.min_transmittance);
     // a wave whose active rays share one direction octant reads that octant's node copy (planes in near / far
     // order, box_hit_nf); waves straddling an axis sign (a few tiles on the lines where a direction component
@@ -510,6 +653,23 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
         if (octw) nbase = a.nodes8 + a.nodes8_stride * oct0;
     }
 
+    // WIDE: the tile's ray bundle -- the range of 1/d over the active rays on each axis (rays that finish later still
+    // lie in it); the wave's copy of the wide nodes is its first active ray's octant
+    [[maybe_unused]] float ilx = 0.f, ihx = 0.f, ily = 0.f, ihy = 0.f, ilz = 0.f, ihz = 0.f;
+    [[maybe_unused]] const WideChild* __restrict__ wbase = nullptr;
+    if constexpr (WIDE) {
+        ilx = wave_minf(active ? inv.x : INFINITY);
+        ihx = wave_maxf(active ? inv.x : -INFINITY);
+        ily = wave_minf(active ? inv.y : INFINITY);
+        ihy = wave_maxf(active ? inv.y : -INFINITY);
+        ilz = wave_minf(active ? inv.z : INFINITY);
+        ihz = wave_maxf(active ? inv.z : -INFINITY);
+        const uint32_t oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
+        const uint64_t am = __builtin_amdgcn_ballot_w64(active);
+        const uint32_t oct0 = (uint32_t)__builtin_amdgcn_readlane((int)oct, am ? (int)__builtin_ctzll(am) : 0);
+        octw = __builtin_amdgcn_ballot_w64(active && oct != oct0) == 0;
+        wbase = a.wide + a.wide_stride * oct0;
+    }
     static_assert(!(LITERAL && PACK), "LITERAL keeps rejected crossings: unpacked k-buffer");
     float kt[KB];
     uint32_t kid[KB];       // record id, or the packed payload (id << 8 | q) when PACK
@@ -544,8 +704,11 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
         if constexpr (LITERAL) {
             if (active && a.max_rounds && rounds >= a.max_rounds) active = false;
         }
-        if constexpr (LITERAL || STATS) {
+        if constexpr (LITERAL) {
             if (active) ++rounds;
+        }
+        if constexpr (STATS) {
+            if (active) ladd(L_ROUNDS);
         }
         // (an inactive lane gets tlo = INF_DIST, so no box test of it can hit and the ballots need no AND with
         // the active mask)
@@ -573,13 +736,99 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
         sp = 0;
         int32_t cur = 0;  // node index (wave-uniform); the node is fetched at the top of each visit so its
                           // 32 SGPRs are not loop-carried
-        if constexpr (STATS) ++w_rounds;
+        wadd(W_ROUNDS, 1);
+        if constexpr (WIDE) {
+            // ---------------- tile-beam traversal of the 64-wide node copies (gvrt_wide.hip).  A node visit is one
+            // coalesced fetch of its 64 children (a child per lane), each tested against the whole ray bundle of the
+            // tile: per axis the slab interval over the bundle's extreme 1/d (the products with both extremes; the
+            // near / far planes of the wave's octant copy, or both planes when the wave straddles an octant), within
+            // the wave's t range [min tlo, max cull distance], widened by the child's acceptance-box D.  Conservative
+            // for every ray of the tile, so no crossing is lost; the leaves then run the exact per-lane test
+            // (GVRT_LEAF).  Hit children are walked in lane order (the octant copy's visiting order): inner ones one
+            // level down (this level's links and remaining mask parked in LDS), leaves in place.
+            const float tlw = wave_minf(active ? tlo : INFINITY);
+            float tcw = wave_maxf(active ? fminf(fminf(thi, kt[KB - 1]), tcut) : 0.0f);
+            int lvl = 0;  // parked levels: nodes on the current path with inner children still to be walked
+            while (true) {
+                if constexpr (STATS) {
+                    wadd(W_NODES, 1);
+                    wadd(W_LATE, s_wst[W_ROUNDS] > 1 ? 1u : 0u);
+                    s_tph[0] = __builtin_amdgcn_s_memtime();
+                }
+                const float4* cp =
+                    reinterpret_cast<const float4*>(wbase + ((uint64_t)(uint32_t)unii(cur) << 6)) + 2 * LL;
+                const float4 c0 = cp[0], c1 = cp[1];
+                int32_t links = __float_as_int(c1.z);  // this lane's child
+                uint64_t hm;
+                {
+                    const float dd = c1.w;
+                    const float an = c0.x - o.x, bf = c0.w - o.x;
+                    const float cn = c0.y - o.y, df = c1.x - o.y;
+                    const float en = c0.z - o.z, ff = c1.y - o.z;
+                    const float a0 = an * ilx, a1 = an * ihx, b0 = bf * ilx, b1 = bf * ihx;
+                    const float c0_ = cn * ily, c1_ = cn * ihy, d0 = df * ily, d1 = df * ihy;
+                    const float e0 = en * ilz, e1 = en * ihz, f0 = ff * ilz, f1 = ff * ihz;
+                    float lx, hx, ly, hy, lz, hz;
+                    if (octw) {  // every ray of the wave has this copy's near planes in n
+                        lx = fminf(a0, a1); hx = fmaxf(b0, b1);
+                        ly = fminf(c0_, c1_); hy = fmaxf(d0, d1);
+                        lz = fminf(e0, e1); hz = fmaxf(f0, f1);
+                    } else {
+                        lx = fminf(fminf(a0, a1), fminf(b0, b1)); hx = fmaxf(fmaxf(a0, a1), fmaxf(b0, b1));
+                        ly = fminf(fminf(c0_, c1_), fminf(d0, d1)); hy = fmaxf(fmaxf(c0_, c1_), fmaxf(d0, d1));
+                        lz = fminf(fminf(e0, e1), fminf(f0, f1)); hz = fmaxf(fmaxf(e0, e1), fmaxf(f0, f1));
+                    }
+                    const float tn = fmaxf(fmaxf(lx, ly), fmaxf(lz, tlw - dd));
+                    const float tf = fminf(fminf(hx, hy), fminf(hz, tcw + dd));
+                    hm = __builtin_amdgcn_ballot_w64(links != WIDE_EMPTY && tn <= tf + 2e-6f * fabsf(tf));
+                }
+                uint64_t lm = hm & __builtin_amdgcn_ballot_w64(links < 0 && links != WIDE_EMPTY);
+                uint64_t im = hm & ~lm;
+                if constexpr (STATS) {
+                    const uint64_t t = __builtin_amdgcn_s_memtime();
+                    wadd(C_NODE, t - s_tph[0]);
+                    s_tph[1] = t;
+                }
+                // ---- the node's leaves first (in visiting order), as the packet traversal does
+#pragma unroll 1
+                while (lm) {
+                    const int j = (int)__builtin_ctzll(lm);
+                    lm &= lm - 1;
+                    GVRT_LEAF(~__builtin_amdgcn_readlane(links, j), __builtin_amdgcn_ballot_w64(active))
+                }
+                if constexpr (STATS) wadd(C_LEAF, __builtin_amdgcn_s_memtime() - s_tph[1]);
+                tcw = wave_maxf(active ? fminf(fminf(thi, kt[KB - 1]), tcut) : 0.0f);
+                // ---- then its first hit inner child; the others parked for later, or the next parked one
+                int32_t next = -1;
+                if (im) {
+                    const int j = (int)__builtin_ctzll(im);
+                    im &= im - 1;
+                    next = __builtin_amdgcn_readlane(links, j);
+                    if (im) {
+                        s_wlink[lvl][LL] = links;
+                        s_wmask[lvl] = im;
+                        ++lvl;
+                    }
+                } else if (lvl > 0) {
+                    const int l = lvl - 1;
+                    const int32_t pl = s_wlink[l][LL];
+                    const uint64_t mm = s_wmask[l];
+                    uint64_t pm = ((uint64_t)uni((uint32_t)(mm >> 32)) << 32) | uni((uint32_t)mm);
+                    const int j = (int)__builtin_ctzll(pm);
+                    pm &= pm - 1;
+                    next = __builtin_amdgcn_readlane(pl, j);
+                    if (pm) s_wmask[l] = pm;
+                    else lvl = l;
+                }
+                if (next < 0) break;
+                cur = next;
+            }
+        } else
         while (true) {
-            [[maybe_unused]] uint64_t t_node0 = 0;
             if constexpr (STATS) {
-                ++w_nodes;
-                w_late += w_rounds > 1 ? 1u : 0u;
-                t_node0 = __builtin_amdgcn_s_memtime();  // the node phase includes the fetch
+                wadd(W_NODES, 1);
+                wadd(W_LATE, s_wst[W_ROUNDS] > 1 ? 1u : 0u);
+                s_tph[0] = __builtin_amdgcn_s_memtime();  // the node phase includes the fetch
             }
             const NodeS nd = load_node_at(nbase, unii(cur));  // whole node: 2x s_load_dwordx16
             float tc = fminf(fminf(thi, kt[KB - 1]), tcut);
@@ -620,7 +869,7 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
             uint32_t hm = 0;
 #pragma unroll
             for (int k = 0; k < BVH_W; ++k) hm |= nz_bit(bal[k], 1u << k);
-            if constexpr (STATS) w_dead += hm == 0 ? 1u : 0u;
+            if constexpr (STATS) wadd(W_DEAD, hm == 0 ? 1u : 0u);
             const uint32_t inner = uni(NODE_PAD(nd, 1));
             uint32_t leafmask = hm & ~inner;
             uint32_t im = hm & inner;
@@ -638,98 +887,19 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
             } else if (sp > 0) {
                 next = pop();
             }
-            [[maybe_unused]] uint64_t t_leaf0 = 0;
             if constexpr (STATS) {
-                t_leaf0 = __builtin_amdgcn_s_memtime();
-                cyc_node += t_leaf0 - t_node0;
+                const uint64_t t = __builtin_amdgcn_s_memtime();
+                wadd(C_NODE, t - s_tph[0]);
+                s_tph[1] = t;
             }
             // ---- leaves of this node (the k-buffer orders them); one rolled loop = one insertion site
 #pragma unroll 1
             while (leafmask) {
                 const int k = __builtin_ctz(leafmask);
                 leafmask &= leafmask - 1;
-                const uint64_t bk = GVRT_PICK(bal, k);
-                const int32_t li = ~GVRT_PICK(ch, k);  // leaf slot
-                const RenderRec rec = load_rec_at(recw, unii(li));
-                // split (SplitBLAS analogue): the piece's proxy id and cell; cell == ~0u admits every crossing
-                uint4 pa = make_uint4((uint32_t)li, 0xFFFFFFFFu, 0u, 0u);
-                if (aux_) pa = aux_[li];
-                {
-                    const uint32_t gi = uni(pa.x);
-                    if constexpr (STATS) ++w_leaves;
-                    if (__builtin_amdgcn_inverse_ballot_w64(bk)) {  // exec &= bk: no per-lane bit test
-                        if constexpr (STATS) ++l_leaves;
-                        // ---- leaf: response (processHit's math) + analytic icosahedron clip
-                        f3 ok, dk;
-                        kernel_frame<OKREC, true>(rec, o, d, ok, dk);
-                        // Conservative pre-reject: gres > hitMinGaussianResponse needs the squared line
-                        // distance gd = |dk x ok|^2 / |dk|^2 below sqrt(ln(minResponse)/S) (a.gpre carries a
-                        // 1e-3 margin), so most proxies are rejected without the sqrt / exp below.
-                        const float l2 = len2(dk);
-                        const f3 cu = cross3(dk, ok);
-                        const bool maybe = (cu.x * cu.x + cu.y * cu.y + cu.z * cu.z) < a.gpre * l2;
-                        bool acc = false;
-                        float galpha = 0.0f;
-                        if (maybe) acc = particle_alpha(ok, dk, l2, rec.density, a.min_response, a.alpha_min, galpha);
-                        if (LITERAL || acc) {
-                            const float hk =
-                                ADAPTIVE ? kernel_scale(rec.density, a.kmin, a.kopts, a.kdeg) * SQRT3 : a.kernel_h;
-                            float tn, tf;
-                            ico_clip(ok, dk, hk, tn, tf);
-                            if (tn <= tf) {
-                                const float al = acc ? galpha : -1.0f;
-                                // (an inclusive tmin exists only in LITERAL mode: the API refuses it otherwise)
-                                const bool incl = LITERAL && a.tmin_inclusive;
-                                bool in0 = (incl ? tn >= tlo : tn > tlo) && tn <= thi;
-                                bool in1 = (incl ? tf >= tlo : tf > tlo) && tf <= thi;
-                                if (uni(pa.y) != 0xFFFFFFFFu) {
-                                    in0 = in0 && crossing_cell(o, d, tn, a, pa.z, pa.w) == pa.y;
-                                    in1 = in1 && crossing_cell(o, d, tf, a, pa.z, pa.w) == pa.y;
-                                }
-                                const float ta = in0 && tn < tcut ? tn : (in1 && tf < tcut ? tf : INF_DIST);
-                                const float tb = (in0 && in1 && tf < tcut) ? tf : INF_DIST;
-                                if (ta < kt[KB - 1]) {
-                                  if constexpr (PACK) {
-                                    const uint32_t q = alpha_code(galpha);
-                                    kb_insert2p<KB>(ta, tb, (gi << 8) | q, kt, kid);
-                                    // termination cull on the q codes (see kb_insert2p): the first slot
-                                    // whose running sum reaches qneed is the last one composited; no
-                                    // slot can reach it while the inserted total is still below
-                                    qtot += tb < INF_DIST ? 2 * q : q;
-                                    if (__builtin_amdgcn_ballot_w64(qtot >= qneed)) {
-                                    uint32_t qs = 0;
-                                    float tt = INF_DIST;
-#pragma unroll
-                                    for (int i = 0; i < KB; ++i) {
-                                        qs += kid[i] & 0xFFu;
-                                        tt = fminf(tt, qs >= qneed ? kt[i] : INF_DIST);
-                                    }
-                                    tcut = fminf(tcut, tt);
-                                    }
-                                  } else {
-                                    kb_insert2<KB>(ta, tb, gi, al, kt, kid, ka);
-                                    // Termination-aware cull distance: walking the sorted slots with the
-                                    // composite's T update, the first slot after which T <= minTransmittance
-                                    // is the last one that can ever be composited (the loop ends there), so
-                                    // nothing farther is needed.  The 1e-4 margin keeps the bound
-                                    // conservative against ulp differences from the composite's arithmetic.
-                                    float Tp = s_T[LL], tt = INF_DIST;
-                                    const float term_cut = a.min_transmittance * 0.9999f;
-                        #pragma unroll
-                                    for (int i = 0; i < KB; ++i) {
-                                        const bool acc_i = kid[i] != INVALID_ID && ka[i] > 0.0f;
-                                        Tp = acc_i ? Tp * (1.0f - ka[i]) : Tp;
-                                        tt = (tt == INF_DIST && acc_i && Tp < term_cut) ? kt[i] : tt;
-                                    }
-                                    tcut = fminf(tcut, tt);
-                                  }
-                                }
-                            }
-                        }
-                    }
-                }
+                GVRT_LEAF(~GVRT_PICK(ch, k), GVRT_PICK(bal, k))  // leaf slot, lanes whose ray hits its box
             }
-            if constexpr (STATS) cyc_leaf += __builtin_amdgcn_s_memtime() - t_leaf0;
+            if constexpr (STATS) wadd(C_LEAF, __builtin_amdgcn_s_memtime() - s_tph[1]);
             if (next < 0) break;
             cur = next;  // uniform by construction; readfirstlane at the load lets the compiler see it
         }
@@ -760,7 +930,7 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                     for (int j = 0; j < CUN; ++j) {
                         go = go && kid[j] != INVALID_ID && T > a.min_transmittance;
                         if (!go) continue;
-                        if constexpr (STATS) ++nproc;
+                        ladd(L_NPROC);
                         uint32_t hid;
                         float halpha;
                         bool hacc;
@@ -838,7 +1008,7 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                 s_acc[LL] = acc;
             }
         }
-        if constexpr (STATS) cyc_comp += __builtin_amdgcn_s_memtime() - t_comp0;
+        if constexpr (STATS) wadd(C_COMP, __builtin_amdgcn_s_memtime() - t_comp0);
     }
 #undef LL
 
@@ -882,27 +1052,28 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
         atomicAdd(a.tile_hist + b, 1u);
     }
     if constexpr (STATS) {
-        unsigned long long s0 = nproc, s1 = ovalid ? (uint32_t)(calpha - a.alpha_init) : 0u, s2 = rounds, s5 = l_leaves;
+        unsigned long long s0 = s_lst[L_NPROC][olane], s1 = ovalid ? (uint32_t)(calpha - a.alpha_init) : 0u,
+                           s2 = s_lst[L_ROUNDS][olane], s5 = s_lst[L_LEAVES][olane];
         for (int off = 32; off > 0; off >>= 1) {
             s0 += __shfl_xor(s0, off);
             s1 += __shfl_xor(s1, off);
             s2 += __shfl_xor(s2, off);
             s5 += __shfl_xor(s5, off);
         }
-        if (lane == 0) {
+        if (olane == 0) {
             atomicAdd(stats_ + 0, s0);
             atomicAdd(stats_ + 1, s1);
             atomicAdd(stats_ + 2, s2);
-            atomicAdd(stats_ + 3, (unsigned long long)w_nodes);
-            atomicAdd(stats_ + 4, (unsigned long long)w_leaves);
+            atomicAdd(stats_ + 3, s_wst[W_NODES]);
+            atomicAdd(stats_ + 4, s_wst[W_LEAVES]);
             atomicAdd(stats_ + 5, s5);
-            atomicAdd(stats_ + 6, (unsigned long long)cyc_node);
-            atomicAdd(stats_ + 7, (unsigned long long)cyc_leaf);
-            atomicAdd(stats_ + 8, (unsigned long long)cyc_comp);
-            atomicAdd(stats_ + 9, (unsigned long long)(__builtin_amdgcn_s_memtime() - cyc_start));
-            atomicAdd(stats_ + 10, (unsigned long long)w_dead);
-            atomicAdd(stats_ + 11, (unsigned long long)w_rounds);
-            atomicAdd(stats_ + 12, (unsigned long long)w_late);
+            atomicAdd(stats_ + 6, s_wst[C_NODE]);
+            atomicAdd(stats_ + 7, s_wst[C_LEAF]);
+            atomicAdd(stats_ + 8, s_wst[C_COMP]);
+            atomicAdd(stats_ + 9, (unsigned long long)(__builtin_amdgcn_s_memtime() - s_tph[2]));
+            atomicAdd(stats_ + 10, s_wst[W_DEAD]);
+            atomicAdd(stats_ + 11, s_wst[W_ROUNDS]);
+            atomicAdd(stats_ + 12, s_wst[W_LATE]);
         }
     }
 }
@@ -950,6 +1121,16 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
                                   0u, a, KARGS);                                                                \
     } while (0)
 #define GVRT_LAUNCH_SO(L, A, K, P, S, O) GVRT_LAUNCH_SOC(L, A, K, P, S, O, false)
+    // the tile-beam traversal of the wide node copies (option GVRT_OPT_WIDE_NODES, render_impl sets a.wide)
+#define GVRT_LAUNCH_W(O)                                                                                          \
+    do {                                                                                                          \
+        if (a.stats)                                                                                              \
+            hipExtLaunchKernelGGL((k_render<false, false, K_FAST_DEFAULT, true, true, false, O, false, true>), g, b, 0, \
+                                  c->stream, ev_start, ev_stop, 0u, a, KARGS);                                    \
+        else                                                                                                      \
+            hipExtLaunchKernelGGL((k_render<false, false, K_FAST_DEFAULT, false, true, false, O, false, true>), g, b, \
+                                  0, c->stream, ev_start, ev_stop, 0u, a, KARGS);                                 \
+    } while (0)
 #define GVRT_LAUNCH(L, A, K, P) GVRT_LAUNCH_SO(L, A, K, P, true, false)
     // FAST packed kernels also come without the per-child box slack, used when the absolute box padding
     // covers the plane rounding for this launch's cameras (RenderArgs::box_exact, set by render_impl)
@@ -981,7 +1162,10 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
                 // the default depth also reads kernel-frame origins from the records when render_impl
                 // prepared them for a single-origin launch (RenderArgs::okrec)
                 // (one record copy per camera for a multi-origin launch: RenderArgs::recs_cam_stride)
-                if (a.okrec && a.recs_cam_stride) {
+                if (a.wide && !a.recs_cam_stride) {
+                    if (a.okrec) GVRT_LAUNCH_W(true);
+                    else GVRT_LAUNCH_W(false);
+                } else if (a.okrec && a.recs_cam_stride) {
                     if (a.box_exact) GVRT_LAUNCH_SOC(false, false, K_FAST_DEFAULT, true, false, true, true);
                     else GVRT_LAUNCH_SOC(false, false, K_FAST_DEFAULT, true, true, true, true);
                 } else if (a.okrec && a.box_exact) GVRT_LAUNCH_SO(false, false, K_FAST_DEFAULT, true, false, true);
@@ -994,6 +1178,7 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
 #undef GVRT_LAUNCH_F
 #undef GVRT_LAUNCH_SO
 #undef GVRT_LAUNCH_SOC
+#undef GVRT_LAUNCH_W
 #undef KARGS
     GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;
@@ -1144,6 +1329,24 @@ __global__ __launch_bounds__(256) void k_rec_origin(uint64_t m, const RenderRec*
     r.py = ok.y;
     r.pz = ok.z;
     dst[i] = r;
+}
+
+// Adaptive enclosing (opts & 1): each leaf's icosahedron half-width sqrt(3) kernelScale(density) -- what the leaf
+// test computed per visit before (powf / logf: 36 B of scratch per lane in the render kernel)
+__global__ __launch_bounds__(256) void k_leaf_hk(uint64_t m, const RenderRec* __restrict__ recs, float kmin,
+                                                 uint32_t kopts, float kdeg, float* __restrict__ hk) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    hk[i] = kernel_scale(recs[i].density, kmin, kopts, kdeg) * SQRT3;
+}
+
+gvrt_status gvrt_launch_leaf_hk(gvrt_context* c) {
+    const uint64_t m = c->n_leaves;
+    if (!m) return GVRT_OK;
+    hipLaunchKernelGGL(k_leaf_hk, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, c->stream, m, c->d_recs,
+                       c->enc.kernel_min_response, c->enc.opts, c->enc.degree, c->d_leaf_hk);
+    GVRT_HIP(c, hipGetLastError());
+    return GVRT_OK;
 }
 
 // Multi-origin launches (a light-field rig): one record copy per camera, copy c holding camera c's origins
