@@ -818,9 +818,9 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         ord_radius = std::max(ord_radius, (int)c->opt[GVRT_OPT_ORDER_SPREAD]);
         std::memcpy(c->ord_prev_vi, view_inverse, 64);
         c->ord_prev_valid = true;
+        if (!tiles) a.tiles = c->d_tcode;
         a.tile_bucket = c->d_tbucket;
         a.tile_hist = c->d_thist + TILE_BUCKETS * c->ord_parity;
-        if (!tiles) a.tiles = c->d_tcode;
         // a camera that moved by more than 12 tiles in one frame: the previous costs say little, supertile order
         if (c->ord_ready && ord_radius <= 12) a.perm = c->d_order;
     }

@@ -653,21 +653,34 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
         if (octw) nbase = a.nodes8 + a.nodes8_stride * oct0;
     }
 
-    // WIDE: the tile's ray bundle -- the range of 1/d over the active rays on each axis (rays that finish later still
-    // lie in it); the wave's copy of the wide nodes is its first active ray's octant
-    [[maybe_unused]] float ilx = 0.f, ihx = 0.f, ily = 0.f, ihy = 0.f, ilz = 0.f, ihz = 0.f;
+    // WIDE: the tile's ray bundle -- the pyramid through the origin spanned by the directions of the tile's corner
+    // lanes (0, 7, 63, 56: every ray of the 8x8 tile is a convex combination of them, the projection being linear in
+    // NDC), as 4 inward plane normals (wave-uniform, in SGPRs); the wave's copy of the wide nodes is its first active
+    // ray's octant (the visiting order)
+    [[maybe_unused]] float pn[4][3] = {};
     [[maybe_unused]] const WideChild* __restrict__ wbase = nullptr;
     if constexpr (WIDE) {
-        ilx = wave_minf(active ? inv.x : INFINITY);
-        ihx = wave_maxf(active ? inv.x : -INFINITY);
-        ily = wave_minf(active ? inv.y : INFINITY);
-        ihy = wave_maxf(active ? inv.y : -INFINITY);
-        ilz = wave_minf(active ? inv.z : INFINITY);
-        ihz = wave_maxf(active ? inv.z : -INFINITY);
+        f3 cd[4];
+        const int cl[4] = {0, 7, 63, 56};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            cd[k] = mk3(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.x), cl[k])),
+                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.y), cl[k])),
+                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.z), cl[k])));
+        const f3 ctr = cd[0] + cd[1] + cd[2] + cd[3];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            f3 n = cross3(cd[k], cd[(k + 1) & 3]);
+            const float nl = sqrtf(dot3(n, n));
+            n = n * (nl > 0.0f ? 1.0f / nl : 0.0f);  // a degenerate pair (a one-pixel-wide frame) culls nothing
+            if (dot3(n, ctr) < 0.0f) n = n * -1.0f;
+            pn[k][0] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(n.x)));
+            pn[k][1] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(n.y)));
+            pn[k][2] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(n.z)));
+        }
         const uint32_t oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
         const uint64_t am = __builtin_amdgcn_ballot_w64(active);
         const uint32_t oct0 = (uint32_t)__builtin_amdgcn_readlane((int)oct, am ? (int)__builtin_ctzll(am) : 0);
-        octw = __builtin_amdgcn_ballot_w64(active && oct != oct0) == 0;
         wbase = a.wide + a.wide_stride * oct0;
     }
     static_assert(!(LITERAL && PACK), "LITERAL keeps rejected crossings: unpacked k-buffer");
@@ -761,26 +774,33 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                 int32_t links = __float_as_int(c1.z);  // this lane's child
                 uint64_t hm;
                 {
+                    // the child box against the tile's pyramid: outside if every corner lies outside one side plane
+                    // (the corner furthest along the plane normal, per axis the larger of the two plane products);
+                    // and against the wave's t range by the box's nearest / farthest distance from the origin (rays
+                    // are unit length: t is distance).  A relative 1e-4 of the box's distance absorbs the rounding of
+                    // the normals.  Conservative for every ray of the tile; the leaves test each ray exactly.
                     const float dd = c1.w;
-                    const float an = c0.x - o.x, bf = c0.w - o.x;
-                    const float cn = c0.y - o.y, df = c1.x - o.y;
-                    const float en = c0.z - o.z, ff = c1.y - o.z;
-                    const float a0 = an * ilx, a1 = an * ihx, b0 = bf * ilx, b1 = bf * ihx;
-                    const float c0_ = cn * ily, c1_ = cn * ihy, d0 = df * ily, d1 = df * ihy;
-                    const float e0 = en * ilz, e1 = en * ihz, f0 = ff * ilz, f1 = ff * ihz;
-                    float lx, hx, ly, hy, lz, hz;
-                    if (octw) {  // every ray of the wave has this copy's near planes in n
-                        lx = fminf(a0, a1); hx = fmaxf(b0, b1);
-                        ly = fminf(c0_, c1_); hy = fmaxf(d0, d1);
-                        lz = fminf(e0, e1); hz = fmaxf(f0, f1);
-                    } else {
-                        lx = fminf(fminf(a0, a1), fminf(b0, b1)); hx = fmaxf(fmaxf(a0, a1), fmaxf(b0, b1));
-                        ly = fminf(fminf(c0_, c1_), fminf(d0, d1)); hy = fmaxf(fmaxf(c0_, c1_), fmaxf(d0, d1));
-                        lz = fminf(fminf(e0, e1), fminf(f0, f1)); hz = fmaxf(fmaxf(e0, e1), fmaxf(f0, f1));
+                    const float ux = c0.x - o.x, vx = c0.w - o.x;
+                    const float uy = c0.y - o.y, vy = c1.x - o.y;
+                    const float uz = c0.z - o.z, vz = c1.y - o.z;
+                    const float mx = fmaxf(fabsf(ux), fabsf(vx)), my = fmaxf(fabsf(uy), fabsf(vy)),
+                                mz = fmaxf(fabsf(uz), fabsf(vz));
+                    const float slack = -1e-4f * (mx + my + mz);
+                    bool in = true;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const float sk = fmaxf(pn[k][0] * ux, pn[k][0] * vx) + fmaxf(pn[k][1] * uy, pn[k][1] * vy) +
+                                         fmaxf(pn[k][2] * uz, pn[k][2] * vz);
+                        in = in && sk >= slack;
                     }
-                    const float tn = fmaxf(fmaxf(lx, ly), fmaxf(lz, tlw - dd));
-                    const float tf = fminf(fminf(hx, hy), fminf(hz, tcw + dd));
-                    hm = __builtin_amdgcn_ballot_w64(links != WIDE_EMPTY && tn <= tf + 2e-6f * fabsf(tf));
+                    // nearest point: per axis the distance of 0 from [min(u, v), max(u, v)]
+                    const float gx = fmaxf(0.0f, fmaxf(fminf(ux, vx), -fmaxf(ux, vx)));
+                    const float gy = fmaxf(0.0f, fmaxf(fminf(uy, vy), -fmaxf(uy, vy)));
+                    const float gz = fmaxf(0.0f, fmaxf(fminf(uz, vz), -fmaxf(uz, vz)));
+                    const float tfar = tcw + dd, tnear = fmaxf(tlw - dd, 0.0f);
+                    const float dmin2 = gx * gx + gy * gy + gz * gz, dmax2 = mx * mx + my * my + mz * mz;
+                    in = in && dmin2 <= tfar * tfar * 1.0001f && dmax2 * 1.0001f >= tnear * tnear;
+                    hm = __builtin_amdgcn_ballot_w64(links != WIDE_EMPTY && in);
                 }
                 uint64_t lm = hm & __builtin_amdgcn_ballot_w64(links < 0 && links != WIDE_EMPTY);
                 uint64_t im = hm & ~lm;

@@ -548,8 +548,12 @@ def main():
     # the first frame of a frame size has no previous per-tile costs: it is dispatched in supertile order
     # (frame 0, rendered synchronously and timed on its own; the handle orders every later frame)
     first_buf = torch.zeros((part_sizes[0],) + item_shape, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    t_ff = time.perf_counter()
     r.render_device(next_vi(), pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=first_buf.data_ptr(),
                     packed=packed)
+    torch.cuda.synchronize()
+    first_frame_wall_ms = (time.perf_counter() - t_ff) * 1e3  # includes a probe launch (option probe_order)
     first_frame_ms = r.render_ms()
     del first_buf
     for _ in range(args.warmup):
@@ -807,6 +811,7 @@ def main():
                             f"cost order of each frame from its predecessor)" if args.camera_path == "orbit"
                             else "static: every frame the config camera"),
             "first_frame_kernel_ms": round(first_frame_ms, 4),
+            "first_frame_wall_ms": round(first_frame_wall_ms, 4),
             "enclose_ms": round(st0["enclose_ms"], 3),
             "accel_ms": round(st0["accel_ms"], 3),
             "first_build_ms": round(first_build["enclose_ms"] + first_build["accel_ms"], 3),

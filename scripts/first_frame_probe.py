@@ -6,8 +6,10 @@ Per config: the measured per-tile cost classes of the static frame (gvrt_read_ti
 FAST hit counts of every pixel, and the same for a 2-degree-moved camera (the orbit step).  Candidate proxies of a
 tile's cost: the accepted-hit count of its centre ray (a 1-ray-per-tile pre-pass would measure it), the mean / max of
 its 4 corner-and-centre rays, the mean over all its 64 rays, and the previous (moved) frame's class spread by the
-motion radius.  Each is scored by its Spearman correlation with the measured cost and by the list-scheduling
-makespan (measured costs dispatched in the proxy's order over 4096 wave slots) over the balanced bound."""
+motion radius, and a low-resolution probe render (one ray per tile centre: what a pre-pass would measure, with its
+kernel time).  Each is scored by its Spearman correlation with the measured cost and by the list-scheduling makespan
+(measured costs dispatched in the proxy's order over 4096 wave slots) over the balanced bound.  Round 4 also built the
+probe pre-pass into the library (an option, since removed): profiles/r04/first_frame_probe.json "first_frames"."""
 import heapq
 import importlib
 import json
@@ -72,6 +74,16 @@ def main():
                 res[tag + "_classes"] = r.tile_costs(W, H)[0].astype(np.float64)
                 res[tag + "_hits"] = img["hit_counts"].reshape(H, W).astype(np.float64)
                 res[tag + "_ms"] = r.render_ms()
+            # a low-resolution probe: one ray per 8x8 tile through its centre (pixel_offset 0.5 at W/8 x H/8: the
+            # same NDC as full-resolution pixel 8i + 4), its accepted-hit counts as the tile cost proxy; its kernel
+            # time is what a probe pass would cost (first launch unordered, then ordered)
+            vi, pi = gv.scene.mipnerf_camera(W, H)
+            probe_ms = []
+            for _ in range(3):
+                lo = r.render(vi, pi, tx_n, ty_n, rgba32f=False, hit_counts=True, pixel_offset=0.5)
+                probe_ms.append(r.render_ms())
+            res["probe_hits"] = lo["hit_counts"].reshape(ty_n, tx_n).astype(np.float64)
+            res["probe_ms"] = probe_ms
             # the first frame of the static camera (no previous costs): supertile order
             r.set_option("tile_order", 0)
             vi, pi = gv.scene.mipnerf_camera(W, H)
@@ -93,7 +105,14 @@ def main():
                "five_mean_hits": score(cost, five.mean(-1).reshape(-1)),
                "five_max_hits": score(cost, five.max(-1).reshape(-1)),
                "tile_mean_hits": score(cost, t.mean(axis=(1, 3)).reshape(-1)),
-               "prev_2deg_classes": score(cost, prev.reshape(-1))}
+               "prev_2deg_classes": score(cost, prev.reshape(-1)),
+               "probe_hits": score(cost, res["probe_hits"].reshape(-1)),
+               "probe_kernel_ms": res["probe_ms"]}
+        from scipy.ndimage import maximum_filter, uniform_filter
+        ph = res["probe_hits"]
+        rec["probe_hits_max3"] = score(cost, maximum_filter(ph, size=3).reshape(-1))
+        rec["probe_hits_mean3"] = score(cost, uniform_filter(ph, size=3).reshape(-1))
+        rec["probe_hits_plus_max3"] = score(cost, (ph + maximum_filter(ph, size=3)).reshape(-1))
         # the supertile order as a proxy: position p gets proxy -p
         st = supertile_order(tx_n, ty_n)
         prox = np.empty(len(st))

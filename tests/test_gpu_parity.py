@@ -770,3 +770,4 @@ def test_wide_nodes_traversal(gv, O, config1, config1_enc):
     for k, az in enumerate((30.0, 30.0, 95.0, 200.0)):
         v2, p2 = gv.scene.mipnerf_camera(W, H, azimuth_deg=az)
         _fast_vs_literal(O, e, frames[1][k], frames[0][k], v2, p2, W, H)
+
