@@ -267,7 +267,6 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
     c->okrecs_nomem = c->recs_cams_nomem = false;
     c->leaf_hk_ok = false;
     gvrt_dfree(c, (void**)&c->d_leaf_hk);
-    c->wide_ok = false;
     gvrt_dfree(c, (void**)&c->d_nodes4x8);
     gvrt_dfree(c, (void**)&c->d_nodes4e);
     gvrt_dfree(c, (void**)&c->d_nodes4ex8);
@@ -696,22 +695,6 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         if (c->accept_ok) {
             a.nodes = c->d_nodes4e;
             a.nodes8 = c->opt[GVRT_OPT_OCTANT_NODES] ? c->d_nodes4ex8 : nullptr;
-        }
-    }
-    // Tile-beam traversal of the 64-wide node copies (option GVRT_OPT_WIDE_NODES): FAST launches at the default depth,
-    // built on first use after a build (and when the acceptance thresholds change); a copy that does not fit, or a
-    // tree deeper than the kernel's level buffers, leaves the launch on the packet traversal
-    if (c->opt[GVRT_OPT_WIDE_NODES] && p->mode == GVRT_MODE_FAST && a.kfast == (uint32_t)K_FAST_DEFAULT &&
-        !(c->enc.opts & 1u) && a.nrecs < 0xFFFFFFu && c->opt[GVRT_OPT_PACKED_KBUFFER] && !c->split_cells) {
-        const bool acc = c->opt[GVRT_OPT_ACCEPT_BOXES] && (p->hit_min_gaussian_response > 0.0f || p->alpha_min > 0.0f);
-        if (!c->wide_ok || c->wide_accept != acc ||
-            (acc && (c->wide_key[0] != p->hit_min_gaussian_response || c->wide_key[1] != p->alpha_min))) {
-            GVRT_HIP(c, hipStreamSynchronize(c->stream));  // queued launches may read the copies being replaced
-            if ((s = gvrt_build_wide(c, acc, p->hit_min_gaussian_response, p->alpha_min))) return s;
-        }
-        if (c->wide_ok) {
-            a.wide = c->d_wide;
-            a.wide_stride = c->n_wide * WIDE_W;
         }
     }
     // Single-origin FAST launches at the default depth read each leaf's kernel-frame origin ok from its record:

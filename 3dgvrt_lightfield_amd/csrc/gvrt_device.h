@@ -58,21 +58,6 @@ struct alignas(16) Bvh4Node {  // (name kept from the 4-wide layout; BVH_W child
 };
 static_assert(sizeof(Bvh4Node) == 28 * BVH_W + 16, "node layout: 128 B (4-wide) / 240 B (8-wide)");
 
-// 64-wide node copies for the tile-beam traversal (gvrt_wide.hip, handle option GVRT_OPT_WIDE_NODES): a wide node is
-// 64 children, one per lane, in the visiting order of one ray-direction octant (8 copies); n / f are the child box's
-// near / far planes for that octant, link >= 0 a wide node, < 0 ~leaf, WIDE_EMPTY an empty slot, d the leaf's
-// acceptance-box widening (0 for inner children and proxy boxes)
-constexpr int WIDE_W = 64;
-constexpr int WIDE_LEVELS = 10;  // levels of the wide tree the kernel's per-level LDS buffers hold
-constexpr int32_t WIDE_EMPTY = (int32_t)0x80000000u;
-struct alignas(16) WideChild {
-    float n[3];
-    float f[3];
-    int32_t link;
-    float d;
-};
-static_assert(sizeof(WideChild) == 32, "wide child: 32 B, two dwordx4 per lane");
-
 
 struct f3 {
     float x, y, z;
@@ -134,8 +119,6 @@ struct RenderArgs {
     uint8_t* tile_bucket;       // per tile-list position: log-scale cost class of its wave, or null
     uint32_t* tile_hist;        // tiles per cost class (TILE_BUCKETS), for the next frame's order
     const float* leaf_hk;       // adaptive enclosing (opts & 1): sqrt(3) x kernelScale(density) per leaf, else null
-    const WideChild* wide;      // wide-node copies (tile-beam traversal), 8 octant copies of wide_stride children
-    uint64_t wide_stride;
 };
 
 // kernelScale, particlePrimitives.comp:81-105

@@ -81,13 +81,6 @@ struct gvrt_context {
     // (the render kernel computing it per leaf visit spilled 36 B per lane)
     float* d_leaf_hk = nullptr;
     bool leaf_hk_ok = false;
-    // 64-wide node copies for the tile-beam traversal (gvrt_wide.hip; option GVRT_OPT_WIDE_NODES), built on the first
-    // launch that uses them after a build, rebuilt when the acceptance thresholds change
-    gvrt::WideChild* d_wide = nullptr;
-    uint64_t wide_cap = 0, n_wide = 0;
-    uint32_t wide_depth = 0;
-    bool wide_ok = false, wide_accept = false;
-    float wide_key[2] = {0.0f, 0.0f};
     uint64_t n_leaves = 0;           // BVH leaves: the survivors, or their split pieces
     uint32_t* d_leaf_aux = nullptr;  // split: per leaf {proxy, cell, proxy's cell range lo, hi} (uint4); else null
     uint32_t split_cells = 0;        // grid cells on the longest axis (0: no split)
@@ -151,7 +144,7 @@ struct gvrt_context {
 
     gvrt_stats stats{};
     // per-handle tuning switches (gvrt_set_option), measured-best defaults
-    int64_t opt[GVRT_OPT_COUNT] = {1, 1, 1, 1, 0, 1, 0, 1, 0, 0};
+    int64_t opt[GVRT_OPT_COUNT] = {1, 1, 1, 1, 0, 1, 0, 1, 0};
 };
 
 gvrt_status gvrt_fail(gvrt_context* c, gvrt_status code, const std::string& msg);
@@ -189,8 +182,6 @@ gvrt_status gvrt_launch_tile_order(gvrt_context* c, const uint32_t* codes, int r
 gvrt_status gvrt_launch_rec_origin(gvrt_context* c, const float* o, gvrt::RenderRec* dst, hipStream_t stream);
 // multi-origin launches: per-camera record copies (dst = ncams x n_leaves records) for the cameras at d_view_inv
 gvrt_status gvrt_launch_rec_cams(gvrt_context* c, uint32_t ncams, const float* d_view_inv, gvrt::RenderRec* dst);
-// gvrt_wide.hip: the 64-wide node copies (d_wide) from the 4-wide nodes, with per-leaf acceptance boxes when `accept`
-gvrt_status gvrt_build_wide(gvrt_context* c, bool accept, float min_response, float alpha_min);
 // adaptive enclosing: d_leaf_hk from the leaf records (k_leaf_hk)
 gvrt_status gvrt_launch_leaf_hk(gvrt_context* c);
 // the 8 octant copies of the 4-wide nodes (d_nodes4x8)

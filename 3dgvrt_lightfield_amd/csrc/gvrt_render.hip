@@ -389,22 +389,6 @@ __device__ inline int launder_lane(int l) {
 }
 __device__ inline uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
-// Wave-wide min / max of a float by DPP (quad permutes, row half-mirror and mirror, then the row broadcasts of
-// GFX9), the result in lane 63 (all 64 lanes take part; callers pass a neutral value for lanes that should not count)
-template <int CTRL, int ROWMASK>
-__device__ inline float dppf(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, ROWMASK, 0xf, false));
-}
-__device__ inline float wave_maxf(float v) {
-    v = fmaxf(v, dppf<0xB1, 0xf>(v));   // quad_perm [1,0,3,2]
-    v = fmaxf(v, dppf<0x4E, 0xf>(v));   // quad_perm [2,3,0,1]
-    v = fmaxf(v, dppf<0x141, 0xf>(v));  // row_half_mirror
-    v = fmaxf(v, dppf<0x140, 0xf>(v));  // row_mirror
-    v = fmaxf(v, dppf<0x142, 0xa>(v));  // row_bcast:15
-    v = fmaxf(v, dppf<0x143, 0xc>(v));  // row_bcast:31
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-}
-__device__ inline float wave_minf(float v) { return -wave_maxf(-v); }
 __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Dispatch geometry.  One wave per workgroup: a finished wave's slot and LDS go to the next tile at once
@@ -412,9 +396,9 @@ __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlan
 // list, workgroups walk ST_W x ST_H supertiles of tiles in row-major order (0.9 / 2.0 / 1.8 % faster than
 // row-major tiles).  4 waves per SIMD (<= 128 VGPRs) measured fastest, ahead of 3 (no spills) and 5 (heavy
 // spills or a smaller k-buffer).
-// One leaf (record li) for the lanes in bk: response, icosahedron clip, k-buffer insertion.  A macro, expanded by the
-// packet and the wide traversal, so that each keeps its own inlined copy (as a lambda capturing the k-buffer by
-// reference the packet kernel spilled 8 B per lane).
+// One leaf (record li) for the lanes in bk: response, icosahedron clip, k-buffer insertion.  A macro (as a lambda
+// capturing the k-buffer by reference the kernel spilled 8 B per lane); round 4's wide-node traversal expanded it
+// too (commit f850e68).
 #define GVRT_LEAF(LI_, BK_)                                                                                        \
     {                                                                                                              \
         const int32_t li = (LI_);                                                                                  \
@@ -506,8 +490,7 @@ _Pragma("unroll")                                                               
 constexpr uint32_t ST_W = 8, ST_H = 4;
 constexpr int RENDER_MIN_WAVES = 4;
 
-template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK, bool SLACK, bool OKREC, bool OKCAM = false,
-          bool WIDE = false>
+template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK, bool SLACK, bool OKREC, bool OKCAM = false>
 __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArgs a, const Bvh4Node* __restrict__ nodes_,
                                                                  const RenderRec* __restrict__ recs_,
                                                                  const RenderRec* __restrict__ crecs_,
@@ -531,11 +514,7 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
     __shared__ float s_tmax[64];
     __shared__ uint32_t s_pxy[64];  // px | py << 16, parked for the output stage (not live in VGPRs)
     __shared__ unsigned long long s_t0;  // wave start (s_memtime), for the per-tile cost class
-    __shared__ int32_t s_stack[WIDE ? 1 : STACK_DEPTH];
-    // WIDE: per level of the wide tree, the links of the visited node's 64 children (lane order = visiting order) and
-    // the mask of its hit children still to be walked
-    __shared__ int32_t s_wlink[WIDE ? WIDE_LEVELS : 1][64];
-    __shared__ unsigned long long s_wmask[WIDE ? WIDE_LEVELS : 1];
+    __shared__ int32_t s_stack[STACK_DEPTH];
     // STATS: the counters live in LDS, not registers (kept in registers they spilled 76-80 B per lane, so the
     // diagnostic build had another register allocation than the shipped kernel): per wave [node visits, leaf visits,
     // node / leaf / composite cycles, dead node visits, rounds, node visits after round 1], per lane [processed
@@ -653,36 +632,6 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
         if (octw) nbase = a.nodes8 + a.nodes8_stride * oct0;
     }
 
-    // WIDE: the tile's ray bundle -- the pyramid through the origin spanned by the directions of the tile's corner
-    // lanes (0, 7, 63, 56: every ray of the 8x8 tile is a convex combination of them, the projection being linear in
-    // NDC), as 4 inward plane normals (wave-uniform, in SGPRs); the wave's copy of the wide nodes is its first active
-    // ray's octant (the visiting order)
-    [[maybe_unused]] float pn[4][3] = {};
-    [[maybe_unused]] const WideChild* __restrict__ wbase = nullptr;
-    if constexpr (WIDE) {
-        f3 cd[4];
-        const int cl[4] = {0, 7, 63, 56};
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            cd[k] = mk3(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.x), cl[k])),
-                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.y), cl[k])),
-                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d.z), cl[k])));
-        const f3 ctr = cd[0] + cd[1] + cd[2] + cd[3];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            f3 n = cross3(cd[k], cd[(k + 1) & 3]);
-            const float nl = sqrtf(dot3(n, n));
-            n = n * (nl > 0.0f ? 1.0f / nl : 0.0f);  // a degenerate pair (a one-pixel-wide frame) culls nothing
-            if (dot3(n, ctr) < 0.0f) n = n * -1.0f;
-            pn[k][0] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(n.x)));
-            pn[k][1] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(n.y)));
-            pn[k][2] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(n.z)));
-        }
-        const uint32_t oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
-        const uint64_t am = __builtin_amdgcn_ballot_w64(active);
-        const uint32_t oct0 = (uint32_t)__builtin_amdgcn_readlane((int)oct, am ? (int)__builtin_ctzll(am) : 0);
-        wbase = a.wide + a.wide_stride * oct0;
-    }
     static_assert(!(LITERAL && PACK), "LITERAL keeps rejected crossings: unpacked k-buffer");
     float kt[KB];
     uint32_t kid[KB];       // record id, or the packed payload (id << 8 | q) when PACK
@@ -750,100 +699,6 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
         int32_t cur = 0;  // node index (wave-uniform); the node is fetched at the top of each visit so its
                           // 32 SGPRs are not loop-carried
         wadd(W_ROUNDS, 1);
-        if constexpr (WIDE) {
-            // ---------------- tile-beam traversal of the 64-wide node copies (gvrt_wide.hip).  A node visit is one
-            // coalesced fetch of its 64 children (a child per lane), each tested against the whole ray bundle of the
-            // tile: per axis the slab interval over the bundle's extreme 1/d (the products with both extremes; the
-            // near / far planes of the wave's octant copy, or both planes when the wave straddles an octant), within
-            // the wave's t range [min tlo, max cull distance], widened by the child's acceptance-box D.  Conservative
-            // for every ray of the tile, so no crossing is lost; the leaves then run the exact per-lane test
-            // (GVRT_LEAF).  Hit children are walked in lane order (the octant copy's visiting order): inner ones one
-            // level down (this level's links and remaining mask parked in LDS), leaves in place.
-            const float tlw = wave_minf(active ? tlo : INFINITY);
-            float tcw = wave_maxf(active ? fminf(fminf(thi, kt[KB - 1]), tcut) : 0.0f);
-            int lvl = 0;  // parked levels: nodes on the current path with inner children still to be walked
-            while (true) {
-                if constexpr (STATS) {
-                    wadd(W_NODES, 1);
-                    wadd(W_LATE, s_wst[W_ROUNDS] > 1 ? 1u : 0u);
-                    s_tph[0] = __builtin_amdgcn_s_memtime();
-                }
-                const float4* cp =
-                    reinterpret_cast<const float4*>(wbase + ((uint64_t)(uint32_t)unii(cur) << 6)) + 2 * LL;
-                const float4 c0 = cp[0], c1 = cp[1];
-                int32_t links = __float_as_int(c1.z);  // this lane's child
-                uint64_t hm;
-                {
-                    // the child box against the tile's pyramid: outside if every corner lies outside one side plane
-                    // (the corner furthest along the plane normal, per axis the larger of the two plane products);
-                    // and against the wave's t range by the box's nearest / farthest distance from the origin (rays
-                    // are unit length: t is distance).  A relative 1e-4 of the box's distance absorbs the rounding of
-                    // the normals.  Conservative for every ray of the tile; the leaves test each ray exactly.
-                    const float dd = c1.w;
-                    const float ux = c0.x - o.x, vx = c0.w - o.x;
-                    const float uy = c0.y - o.y, vy = c1.x - o.y;
-                    const float uz = c0.z - o.z, vz = c1.y - o.z;
-                    const float mx = fmaxf(fabsf(ux), fabsf(vx)), my = fmaxf(fabsf(uy), fabsf(vy)),
-                                mz = fmaxf(fabsf(uz), fabsf(vz));
-                    const float slack = -1e-4f * (mx + my + mz);
-                    bool in = true;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const float sk = fmaxf(pn[k][0] * ux, pn[k][0] * vx) + fmaxf(pn[k][1] * uy, pn[k][1] * vy) +
-                                         fmaxf(pn[k][2] * uz, pn[k][2] * vz);
-                        in = in && sk >= slack;
-                    }
-                    // nearest point: per axis the distance of 0 from [min(u, v), max(u, v)]
-                    const float gx = fmaxf(0.0f, fmaxf(fminf(ux, vx), -fmaxf(ux, vx)));
-                    const float gy = fmaxf(0.0f, fmaxf(fminf(uy, vy), -fmaxf(uy, vy)));
-                    const float gz = fmaxf(0.0f, fmaxf(fminf(uz, vz), -fmaxf(uz, vz)));
-                    const float tfar = tcw + dd, tnear = fmaxf(tlw - dd, 0.0f);
-                    const float dmin2 = gx * gx + gy * gy + gz * gz, dmax2 = mx * mx + my * my + mz * mz;
-                    in = in && dmin2 <= tfar * tfar * 1.0001f && dmax2 * 1.0001f >= tnear * tnear;
-                    hm = __builtin_amdgcn_ballot_w64(links != WIDE_EMPTY && in);
-                }
-                uint64_t lm = hm & __builtin_amdgcn_ballot_w64(links < 0 && links != WIDE_EMPTY);
-                uint64_t im = hm & ~lm;
-                if constexpr (STATS) {
-                    const uint64_t t = __builtin_amdgcn_s_memtime();
-                    wadd(C_NODE, t - s_tph[0]);
-                    s_tph[1] = t;
-                }
-                // ---- the node's leaves first (in visiting order), as the packet traversal does
-#pragma unroll 1
-                while (lm) {
-                    const int j = (int)__builtin_ctzll(lm);
-                    lm &= lm - 1;
-                    GVRT_LEAF(~__builtin_amdgcn_readlane(links, j), __builtin_amdgcn_ballot_w64(active))
-                }
-                if constexpr (STATS) wadd(C_LEAF, __builtin_amdgcn_s_memtime() - s_tph[1]);
-                tcw = wave_maxf(active ? fminf(fminf(thi, kt[KB - 1]), tcut) : 0.0f);
-                // ---- then its first hit inner child; the others parked for later, or the next parked one
-                int32_t next = -1;
-                if (im) {
-                    const int j = (int)__builtin_ctzll(im);
-                    im &= im - 1;
-                    next = __builtin_amdgcn_readlane(links, j);
-                    if (im) {
-                        s_wlink[lvl][LL] = links;
-                        s_wmask[lvl] = im;
-                        ++lvl;
-                    }
-                } else if (lvl > 0) {
-                    const int l = lvl - 1;
-                    const int32_t pl = s_wlink[l][LL];
-                    const uint64_t mm = s_wmask[l];
-                    uint64_t pm = ((uint64_t)uni((uint32_t)(mm >> 32)) << 32) | uni((uint32_t)mm);
-                    const int j = (int)__builtin_ctzll(pm);
-                    pm &= pm - 1;
-                    next = __builtin_amdgcn_readlane(pl, j);
-                    if (pm) s_wmask[l] = pm;
-                    else lvl = l;
-                }
-                if (next < 0) break;
-                cur = next;
-            }
-        } else
         while (true) {
             if constexpr (STATS) {
                 wadd(W_NODES, 1);
@@ -1141,16 +996,6 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
                                   0u, a, KARGS);                                                                \
     } while (0)
 #define GVRT_LAUNCH_SO(L, A, K, P, S, O) GVRT_LAUNCH_SOC(L, A, K, P, S, O, false)
-    // the tile-beam traversal of the wide node copies (option GVRT_OPT_WIDE_NODES, render_impl sets a.wide)
-#define GVRT_LAUNCH_W(O)                                                                                          \
-    do {                                                                                                          \
-        if (a.stats)                                                                                              \
-            hipExtLaunchKernelGGL((k_render<false, false, K_FAST_DEFAULT, true, true, false, O, false, true>), g, b, 0, \
-                                  c->stream, ev_start, ev_stop, 0u, a, KARGS);                                    \
-        else                                                                                                      \
-            hipExtLaunchKernelGGL((k_render<false, false, K_FAST_DEFAULT, false, true, false, O, false, true>), g, b, \
-                                  0, c->stream, ev_start, ev_stop, 0u, a, KARGS);                                 \
-    } while (0)
 #define GVRT_LAUNCH(L, A, K, P) GVRT_LAUNCH_SO(L, A, K, P, true, false)
     // FAST packed kernels also come without the per-child box slack, used when the absolute box padding
     // covers the plane rounding for this launch's cameras (RenderArgs::box_exact, set by render_impl)
@@ -1182,10 +1027,7 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
                 // the default depth also reads kernel-frame origins from the records when render_impl
                 // prepared them for a single-origin launch (RenderArgs::okrec)
                 // (one record copy per camera for a multi-origin launch: RenderArgs::recs_cam_stride)
-                if (a.wide && !a.recs_cam_stride) {
-                    if (a.okrec) GVRT_LAUNCH_W(true);
-                    else GVRT_LAUNCH_W(false);
-                } else if (a.okrec && a.recs_cam_stride) {
+                if (a.okrec && a.recs_cam_stride) {
                     if (a.box_exact) GVRT_LAUNCH_SOC(false, false, K_FAST_DEFAULT, true, false, true, true);
                     else GVRT_LAUNCH_SOC(false, false, K_FAST_DEFAULT, true, true, true, true);
                 } else if (a.okrec && a.box_exact) GVRT_LAUNCH_SO(false, false, K_FAST_DEFAULT, true, false, true);
@@ -1198,7 +1040,6 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
 #undef GVRT_LAUNCH_F
 #undef GVRT_LAUNCH_SO
 #undef GVRT_LAUNCH_SOC
-#undef GVRT_LAUNCH_W
 #undef KARGS
     GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;

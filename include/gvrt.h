@@ -270,10 +270,7 @@ gvrt_status gvrt_get_device_buffers(gvrt_handle h, gvrt_device_buffers* out);
                                        acceptance node copies, record-origin copies) are allocated only while the
                                        handle's device memory stays within N MiB; a copy that does not fit (or
                                        whose hipMalloc fails) is left out and launches run without it */
-#define GVRT_OPT_WIDE_NODES 9u     /* 0 (default): packet traversal of the 4-wide tree; 1 (experiment): FAST launches
-                                       at the default depth traverse 64-wide node copies, all children of a node
-                                       tested at once against the tile's ray bundle */
-#define GVRT_OPT_COUNT 10u
+#define GVRT_OPT_COUNT 9u
 gvrt_status gvrt_set_option(gvrt_handle h, uint32_t option, int64_t value);
 gvrt_status gvrt_get_option(gvrt_handle h, uint32_t option, int64_t* value);
 

@@ -738,36 +738,3 @@ def test_origin_record_copies_queued_moving_camera(gv, config1):
         np.testing.assert_array_equal(b.cpu().numpy().reshape(ref[k].shape), ref[k])
 
 
-def test_wide_nodes_traversal(gv, O, config1, config1_enc):
-    """The tile-beam traversal of the 64-wide node copies (option wide_nodes): the leaves are tested
-    by the same exact per-lane code, only which leaves a wave visits and in which order changes, so the frame matches
-    the oracle under the full accounting, equals the packet traversal's frame on every ray the oracle does not flag
-    (a different arrival order may only swap crossings whose t ties), and does not depend on the acceptance boxes
-    (culling only) -- config 1 and a dense subset, single camera and moving cameras."""
-    W = H = 256
-    vi, pi = gv.scene.config1_camera(W, H)
-    outs = {}
-    for wide, acc in ((0, 1), (1, 1), (1, 0)):
-        with gv.Renderer(0) as r:
-            r.set_option("wide_nodes", wide)
-            r.set_option("accept_boxes", acc)
-            r.prepare(config1, builder=2, collapse=1)
-            outs[(wide, acc)] = r.render(vi, pi, W, H)["rgba32f"]
-    ref = O.render(config1_enc, vi, pi, W, H, proxy_mode=1)
-    _cmp_images(outs[(1, 1)], ref)
-    np.testing.assert_array_equal(outs[(1, 1)], outs[(1, 0)])
-    _fast_vs_literal(O, config1_enc, outs[(1, 1)], outs[(0, 1)], vi, pi, W, H)
-    s = gv.scene.dense_standin(60_000, seed=4)
-    e = O.enclose(s)
-    W, H = 192, 128
-    frames = {}
-    for wide in (0, 1):
-        with gv.Renderer(0) as r:
-            r.set_option("wide_nodes", wide)
-            r.prepare(s, builder=2, collapse=1)
-            frames[wide] = [r.render(*gv.scene.mipnerf_camera(W, H, azimuth_deg=az), W, H)["rgba32f"]
-                            for az in (30.0, 30.0, 95.0, 200.0)]
-    for k, az in enumerate((30.0, 30.0, 95.0, 200.0)):
-        v2, p2 = gv.scene.mipnerf_camera(W, H, azimuth_deg=az)
-        _fast_vs_literal(O, e, frames[1][k], frames[0][k], v2, p2, W, H)
-
