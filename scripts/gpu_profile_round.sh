@@ -1,11 +1,14 @@
 # Full measurement pass for profiles/: GPU tests, smoke, the bench line (PMC passes + CPU baseline), rocprofv3 kernel
 # stats of the same bench command, PMC passes on the render loop, every config's bench line, the moving-camera and
-# rank-balance lines.  usage: TAG=r03 [SKIP_TESTS=1] [PMC_ONLY=1] bash scripts/gpu_profile_round.sh
+# rank-balance lines.  usage: TAG=r04 [SKIP_TESTS=1] [PMC_ONLY=1] [PART=1|2] bash scripts/gpu_profile_round.sh
+# (PART=1: tests, smoke, bench, rocprof stats, PMC passes; PART=2: the other configs' lines and the extra lines --
+# each part fits one gpurun call)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 out=gpurun_out/$TAG
 mkdir -p $out/pmc
+if [ "$PART" != "2" ]; then
 if [ -z "$PMC_ONLY" ]; then
 if [ -z "$SKIP_TESTS" ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $out/pytest_gpu.log 2>&1 || { tail -20 $out/pytest_gpu.log; exit 1; }
@@ -27,8 +30,14 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_I
 done
 python3 scripts/pmc_summary.py $out/pmc > $out/pmc_summary.json && head -30 $out/pmc_summary.json
 [ -n "$PMC_ONLY" ] && exit 0
+fi
+[ "$PART" = "1" ] && exit 0
 for cfg in garden truck lightfield dense; do
   timeout -k 10 300 python bench.py --config $cfg --steps 20 --warmup 3 --no-cpu-baseline > $out/config_$cfg.json 2> $out/config_$cfg.err || { echo "$cfg failed"; tail -5 $out/config_$cfg.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$out/config_$cfg.json')); print('$cfg', d['value'], d['ms_per_step'], d['kernel_ms'], d['roofline']['frac'])"
+  python3 -c "import json; d=json.load(open('$out/config_$cfg.json')); r=d['roofline']; print('$cfg', d['value'], d['ms_per_step'], d['kernel_ms'], r['bound'], r['frac'], r.get('logical', {}).get('frac'), r.get('hbm', {}).get('frac'))"
+done
+for cfg in bicycle dense; do
+  timeout -k 10 200 python3 scripts/orbit_costs_dump.py $out/orbit_costs_$cfg.npz $cfg 0.1 0.5 2 > $out/orbit_costs_$cfg.log 2>&1 || { echo "orbit costs $cfg failed"; tail -5 $out/orbit_costs_$cfg.log; exit 1; }
+  cat $out/orbit_costs_$cfg.log
 done
 BENCH_OUT=$out BENCH_LINES="${EXTRA_LINES:---camera-path orbit --orbit-step 0.5 --steps 40 --no-pmc --no-cpu-baseline --no-stats;--camera-path orbit --orbit-step 2 --steps 40 --no-pmc --no-cpu-baseline --no-stats;--config truck --rank-balance 8 --no-pmc --no-cpu-baseline --no-stats;--config lightfield --rank-balance 8 --no-pmc --no-cpu-baseline --no-stats}" bash scripts/gpu_bench_lines.sh
