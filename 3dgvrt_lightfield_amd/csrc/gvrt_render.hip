@@ -47,8 +47,9 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 
 static_assert(BVH_W == 4, "the render kernel traverses 4-wide nodes");
 
-// Composite tuning (same-box A/B): the first SH_EARLY of a hit's 12 SH float4 loads are
-// consumed before the accept branch, so they are issued with the record's (all 12: spills); the FAST K = 24
+// Composite tuning (same-box A/B): the first SH_EARLY of a hit's 12 SH float4 loads are summed
+// before the accept branch (round 2: issued with the record's, -1.5 %; the ROCm 7.2 compiler sinks them into the
+// branch again, and forcing 3 or 6 of them out with an asm anchor measured +0.5-1 % in round 4); the FAST K = 24
 // buffer is composited in groups of COMP_GROUP slots (static register indices, one buffer shift per group).
 constexpr int SH_EARLY = 6;
 constexpr int COMP_GROUP = 6;
@@ -810,9 +811,8 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                         float halpha;
                         bool hacc;
                         hid = PACK ? (kid[j] >> 8) : kid[j];
-                        // the SH address needs only the id: issue all 12 loads with the record's, one
-                        // memory round trip per hit instead of one per dependent chunk (the first SH_EARLY of
-                        // them are consumed unconditionally, so they are not sunk behind the accept branch)
+                        // the SH address needs only the id: all 12 loads in one batch, one memory round trip
+                        // instead of one per dependent chunk (see SH_EARLY for where the compiler issues them)
                         float4 shv[12];
                         {
                             const float4* s4 = reinterpret_cast<const float4*>(sh_ + 48ull * hid);
