@@ -68,18 +68,26 @@ __global__ __launch_bounds__(256) void k_enclose_flags(uint64_t n, const float* 
     flags[g] = ok ? 1u : 0u;
 }
 
-// SH records [f_dc, f_rest] in compaction order (particlePrimitives.comp:207-214), one thread per
-// output float: consecutive threads write consecutive floats and read consecutive floats of one
-// Gaussian (the 48-float rows of consecutive survivors come from nearly consecutive sources).
+// SH records [f_dc, f_rest] in compaction order (particlePrimitives.comp:207-214): consecutive threads write
+// consecutive float4s and read consecutive floats of one Gaussian (the 48-float rows of consecutive survivors
+// come from nearly consecutive sources).
 __global__ __launch_bounds__(256) void k_enclose_sh(const uint32_t* __restrict__ count, const uint32_t* __restrict__ src,
                                                     const float* __restrict__ fdc, const float* __restrict__ frest,
                                                     float* __restrict__ sh48) {
-    const uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (o >= 48ull * *count) return;  // grid sized for n; the survivor count is scan[n]
-    const uint64_t sidx = o / 48;
-    const uint32_t c = (uint32_t)(o - 48 * sidx);
+    // one thread per output float4 (12 per survivor): aligned 16-B stores, and the 4 input floats of a thread are
+    // consecutive in the survivor's f_dc / f_rest row, so a wave's reads stay row-contiguous
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= 12ull * *count) return;  // grid sized for n; the survivor count is scan[n]
+    const uint64_t sidx = q / 12;
+    const uint32_t c0 = 4 * (uint32_t)(q - 12 * sidx);
     const uint64_t g = src[sidx];
-    sh48[o] = c < 3 ? fdc[3 * g + c] : frest[g * SPEC_DIM + (c - 3)];
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t c = c0 + k;
+        v[k] = c < 3 ? fdc[3 * g + c] : frest[g * SPEC_DIM + (c - 3)];
+    }
+    reinterpret_cast<float4*>(sh48)[q] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
 __device__ __constant__ float c_icosa[12][3] = {
@@ -116,15 +124,22 @@ struct EncloseArgs {
 // Largest finite |position component| of the splats (float bits: non-negative floats order as their bits).
 // The proxy boxes get an absolute padding of 2^-18 x this bound: it covers the rounding of the render
 // kernel's FMA-form box planes for ray origins within 4x the bound, so that kernel needs no per-box slack.
+// One atomic per block: device atomics on one word serialise (~11 ns each on MI355X), so the
+// 8192 per-wave atomics of the first version cost 97 us at 1 M; the grid is capped at 1024 blocks.
 __global__ __launch_bounds__(256) void k_pos_absmax(uint64_t n3, const float* __restrict__ pos,
                                                     uint32_t* __restrict__ out) {
+    __shared__ float s_m[4];
     float m = 0.0f;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n3; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+#pragma unroll 4
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n3; i += stride) {
         const float v = fabsf(pos[i]);
         if (v <= 3.0e38f) m = fmaxf(m, v);  // NaN / inf positions do not set the bound
     }
     for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+    if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]))));
 }
 
 // particlePrimitives.comp:142-214
@@ -281,7 +296,7 @@ gvrt_status gvrt_launch_enclose(gvrt_context* c, const gvrt_enclosing_params* p,
     GVRT_HIP(c, hipMemsetAsync(d_absmax, 0, 4, c->stream));
     {
         const uint64_t n3 = 3 * n;
-        const unsigned rb = (unsigned)std::min<uint64_t>((n3 + 255) / 256, 2048);
+        const unsigned rb = (unsigned)std::min<uint64_t>((n3 + 255) / 256, 1024);
         hipLaunchKernelGGL(k_pos_absmax, dim3(rb), dim3(256), 0, c->stream, n3, c->d_pos, d_absmax);
         e = hipGetLastError();
         if (e != hipSuccess) {
@@ -317,8 +332,8 @@ gvrt_status gvrt_launch_enclose(gvrt_context* c, const gvrt_enclosing_params* p,
         return gvrt_hip_check(c, e, "k_enclose_emit");
     }
     {
-        const uint64_t nf = 48ull * n;
-        hipLaunchKernelGGL(k_enclose_sh, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, c->stream, c->d_scan + n,
+        const uint64_t nq = 12ull * n;
+        hipLaunchKernelGGL(k_enclose_sh, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, c->stream, c->d_scan + n,
                            c->d_src, c->d_fdc, c->d_frest, c->d_sh48);
         e = hipGetLastError();
         if (e != hipSuccess) {

@@ -399,30 +399,37 @@ __global__ __launch_bounds__(256) void k_collapse_level(const BvhNode* __restric
         }
         ++cnt_s;
     }
-    // next-level ids: one atomic per wave (a single counter per level took one atomic per node, all on
-    // one address), lanes offset by an exclusive prefix sum of their internal-child counts
+    // next-level ids: one atomic per block (device atomics on one word serialise, ~11 ns each on MI355X:
+    // one per node, then one per wave, cost tens of microseconds per wide level), lanes offset by an exclusive
+    // prefix sum of their internal-child counts within the block
     uint32_t nin = 0;
     if (live)
         for (int j = 0; j < cnt_s; ++j) nin += ref[j] >= 0 ? 1u : 0u;
-    const int lane = (int)(threadIdx.x & 63);
+    const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
     uint32_t incl = nin;
     for (int off = 1; off < 64; off <<= 1) {
         const uint32_t v = (uint32_t)__shfl_up((int)incl, off, 64);
         if (lane >= off) incl += v;
     }
-    const uint32_t wtotal = (uint32_t)__shfl((int)incl, 63, 64);
-    uint32_t wbase = 0;
-    if (lane == 0 && wtotal) wbase = atomicAdd(cnt + level + 1, wtotal);
-    wbase = (uint32_t)__shfl((int)wbase, 0, 64);
-    // the wave's deepest binary leaf and whether it made any next-level node: one atomic each per wave
+    // the deepest binary leaf below this lane's node
     uint32_t ld = 0;
     if (live)
         for (int j = 0; j < cnt_s; ++j) ld = ref[j] < 0 ? max(ld, rd[j]) : ld;
     for (int off = 32; off > 0; off >>= 1) ld = max(ld, (uint32_t)__shfl_xor((int)ld, off, 64));
-    if (lane == 0) {
-        if (wtotal) atomicMax(ctl + 0, level + 1);
-        if (ld) atomicMax(ctl + 1, ld);
+    __shared__ uint32_t s_wt[4], s_ld[4], s_base;
+    if (lane == 63) s_wt[wave] = incl;
+    if (lane == 0) s_ld[wave] = ld;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t tot = s_wt[0] + s_wt[1] + s_wt[2] + s_wt[3];
+        const uint32_t bld = max(max(s_ld[0], s_ld[1]), max(s_ld[2], s_ld[3]));
+        s_base = tot ? atomicAdd(cnt + level + 1, tot) : 0u;
+        if (tot) atomicMax(ctl + 0, level + 1);  // this level made next-level nodes
+        if (bld) atomicMax(ctl + 1, bld);
     }
+    __syncthreads();
+    uint32_t wbase = s_base;
+    for (int w = 0; w < wave; ++w) wbase += s_wt[w];
     if (!live) return;
     uint32_t next_id = end + wbase + (incl - nin);  // level + 1 starts right after this level
     Bvh4Node o;
