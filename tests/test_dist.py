@@ -1,4 +1,5 @@
-"""Multi-rank frame split + RCCL-style gather, exercised with torch.distributed 'gloo' on CPU (world 2 and 3).
+"""Multi-rank frame split + RCCL-style gather, exercised with torch.distributed 'gloo' on CPU (world 2, 3 and 8:
+the driver's 8-GPU node, config 5 with 16 views over 8 ranks).
 
 The renderer is replaced by a deterministic per-pixel pattern so the test checks what the N>1 path
 owns: tile assignment (disjoint, complete), padding of unequal parts for the gather, the gather
@@ -139,7 +140,8 @@ def _exchange_worker(rank, world, port, split, width, height, views, nframes, q)
 
 
 @pytest.mark.parametrize("world,split,width,height,views", [(2, "tiles", 100, 60, 1), (3, "tiles", 37, 29, 1),
-                                                             (2, "views", 24, 16, 5), (3, "views", 16, 8, 3)])
+                                                             (2, "views", 24, 16, 5), (3, "views", 16, 8, 3),
+                                                             (8, "tiles", 72, 40, 1), (8, "views", 16, 8, 16)])
 def test_frame_exchange_double_buffered(world, split, width, height, views):
     """bench.py's N-rank path on CPU: dist.FrameExchange with two send buffers in flight, unequal parts (tiles:
     ragged block counts; views: 5 views over 2 ranks) sent point to point at their exact sizes (no padding: every
