@@ -275,6 +275,13 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
     gvrt_status s = gvrt_launch_build_accel(c, *p);
     if (s) return s;
     if ((s = gvrt_launch_node_octants(c))) return s;
+    // adaptive enclosing: each leaf's icosahedron half-width, a required array allocated with the build (a render
+    // never allocates it, so a handle that builds also renders without a new out-of-memory point)
+    if ((c->enc.opts & 1u) && c->n_leaves) {
+        if ((s = gvrt_dalloc(c, (void**)&c->d_leaf_hk, 4 * c->n_leaves))) return s;
+        if ((s = gvrt_launch_leaf_hk(c))) return s;
+        c->leaf_hk_ok = true;
+    }
     return GVRT_OK;
 }
 
@@ -303,11 +310,14 @@ gvrt_status gvrt_get_device_properties(int device, gvrt_device_properties* out) 
 
 gvrt_status gvrt_read_accel(gvrt_handle c, int which, void* out, uint64_t cap, uint64_t* count) {
     if (!c || !count) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "NULL argument");
-    if (which != 0 && which != 1) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "which must be 0 (binary) or 1 (4-wide)");
+    if (which < 0 || which > 2)
+        return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "which must be 0 (binary), 1 (4-wide) or 2 (leaf half-widths)");
     if (!c->accel) return gvrt_fail(c, GVRT_ERR_STATE, "gvrt_build_accel has not been called");
-    const uint64_t n = which == 0 ? (c->n_leaves > 1 ? c->n_leaves - 1 : 0) : c->n_nodes4;
-    const void* src = which == 0 ? (const void*)c->d_nodes : (const void*)c->d_nodes4;
-    const uint64_t sz = which == 0 ? sizeof(gvrt::BvhNode) : sizeof(gvrt::Bvh4Node);
+    const uint64_t n = which == 0   ? (c->n_leaves > 1 ? c->n_leaves - 1 : 0)
+                       : which == 1 ? c->n_nodes4
+                                    : (c->leaf_hk_ok ? c->n_leaves : 0);
+    const void* src = which == 0 ? (const void*)c->d_nodes : which == 1 ? (const void*)c->d_nodes4 : (const void*)c->d_leaf_hk;
+    const uint64_t sz = which == 0 ? sizeof(gvrt::BvhNode) : which == 1 ? sizeof(gvrt::Bvh4Node) : sizeof(float);
     *count = n;
     if (!out || !n) return GVRT_OK;
     if (!src) return gvrt_fail(c, GVRT_ERR_STATE, "tree not kept by this build");
@@ -676,18 +686,16 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
                       std::ldexp(omax, -20) <= c->box_pad_abs;  // also false for a NaN origin
     }
     a.kfast = p->kbuffer_depth ? p->kbuffer_depth : (uint32_t)K_FAST_DEFAULT;
-    // adaptive enclosing: the per-leaf icosahedron half-widths, once per build
+    // adaptive enclosing: the per-leaf icosahedron half-widths, written with the build (gvrt_build_accel_ex)
     if ((c->enc.opts & 1u) && c->n_leaves) {
-        if (!c->leaf_hk_ok) {
-            if (!c->d_leaf_hk && (s = gvrt_dalloc(c, (void**)&c->d_leaf_hk, 4 * c->n_leaves))) return s;
-            if ((s = gvrt_launch_leaf_hk(c))) return s;
-            c->leaf_hk_ok = true;
-        }
+        if (!c->leaf_hk_ok) return gvrt_fail(c, GVRT_ERR_STATE, "adaptive enclosing without per-leaf half-widths");
         a.leaf_hk = c->d_leaf_hk;
     }
     // FAST launches traverse the acceptance-box nodes (gvrt_launch_accept_nodes), refit when the acceptance
-    // thresholds change; LITERAL launches keep every crossing and so the proxy boxes
-    if (p->mode == GVRT_MODE_FAST && c->opt[GVRT_OPT_ACCEPT_BOXES] && !c->split_cells &&
+    // thresholds change; LITERAL launches keep every crossing and so the proxy boxes.  A negative alphaMin keeps the
+    // proxy boxes too: a particle of density rho <= alphaMin < 0 is then accepted in a shell (min(0.99, gres rho) >
+    // alphaMin for small gres), not inside a ball, so neither its acceptance ball nor its drop would be exact
+    if (p->mode == GVRT_MODE_FAST && c->opt[GVRT_OPT_ACCEPT_BOXES] && !c->split_cells && p->alpha_min >= 0.0f &&
         (p->hit_min_gaussian_response > 0.0f || p->alpha_min > 0.0f) && a.nrecs < 0xFFFFFFu &&
         c->opt[GVRT_OPT_PACKED_KBUFFER]) {
         if (!c->accept_ok || c->accept_key[0] != p->hit_min_gaussian_response || c->accept_key[1] != p->alpha_min)

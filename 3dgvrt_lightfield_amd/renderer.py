@@ -243,9 +243,15 @@ class Renderer:
 
     def read_accel(self, which=1):
         """gvrt_read_accel: the binary tree (which=0, float32 [n, 16] rows: child boxes, then c0, c1, axis
-        as int32 views) or the 4-wide tree (which=1, [n, 32] rows), as raw 32-bit words (uint32)."""
+        as int32 views), the 4-wide tree (which=1, [n, 32] rows), as raw 32-bit words (uint32), or (which=2,
+        adaptive enclosing) each leaf's icosahedron half-width as float32 [n_leaves]."""
         n = C.c_uint64(0)
         check(lib().gvrt_read_accel(self.h, int(which), None, 0, C.byref(n)), self.h)
+        if which == 2:
+            hk = np.zeros(int(n.value), np.float32)
+            if n.value:
+                check(lib().gvrt_read_accel(self.h, 2, hk.ctypes.data, n.value, C.byref(n)), self.h)
+            return hk
         words = 16 if which == 0 else 32
         out = np.zeros((int(n.value), words), np.uint32)
         if n.value:

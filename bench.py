@@ -86,6 +86,12 @@ def parse():
                     help="N-rank runs (--gpus N > 1, or --exchange): strong-scaling sub-records of these frames "
                          "(bicycle: the config-2 1080p frame, truck: the config-4 4K frame), each tile-split over the "
                          "ranks in cost bands and exchanged to rank 0; 'none' to skip")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the `configs` sub-record of the default one-GPU line (garden, truck 4K, light field, dense, "
+                         "orbit 0.5 deg: kernel ms, Mrays/s, VALU issue, logical fraction, first frame)")
+    ap.add_argument("--configs-child", action="store_true", help=argparse.SUPPRESS)  # PMC child of the configs record
+    ap.add_argument("--pmc-keep", default=None, metavar="DIR",
+                    help="keep the per-dispatch PMC rows of the line's own passes as DIR/bench_pmc.json (profiles/)")
     ap.add_argument("--build", default="quality", choices=["quality", "fast"],
                     help="quality: device binned-SAH tree + SAH-optimal 4-wide collapse (the static-scene build, "
                          "as the reference's PREFER_FAST_TRACE BLAS); fast: device LBVH + greedy collapse")
@@ -127,7 +133,8 @@ def cpu_share():
 # ------------------------------------------------------------------------------------------------ PMC
 def pmc_passes(args):
     """roofline.traffic and the VALU-issue roofline from rocprofv3 PMC passes of THIS command (a short run:
-    5 timed + 1 warmup FAST launches, no CPU baseline / stats), one counter set per pass as MI355X_MICROARCH.md
+    5 timed + 1 warmup FAST launches after the unordered first frame, which is not averaged; no CPU baseline /
+    stats), one counter set per pass as MI355X_MICROARCH.md
     prescribes (FETCH_SIZE and WRITE_SIZE cannot share a pass).  Runs as child processes before this process
     touches the GPU.  Returns per-dispatch averages of the k_render kernel, or {"error": ...}."""
     exe = shutil.which("rocprofv3")
@@ -135,7 +142,7 @@ def pmc_passes(args):
         return {"error": "rocprofv3 not found"}
     child = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", "5", "--warmup", "1",
              "--config", args.config, "--split", args.split, "--mode", args.mode, "--build", args.build,
-             "--no-cpu-baseline", "--no-stats", "--no-pmc"]
+             "--no-cpu-baseline", "--no-stats", "--no-pmc", "--no-configs"]
     if args.ply:
         child += ["--ply", args.ply]
     for kv in args.option:
@@ -143,6 +150,7 @@ def pmc_passes(args):
     if args.camera_path != "static":
         child += ["--camera-path", args.camera_path, "--orbit-step", str(args.orbit_step)]
     out = {}
+    kept = []
     # (8 SQ counters and 1 GRBM counter fit one pass; FETCH_SIZE / WRITE_SIZE need TCC passes of their own)
     passes = [["FETCH_SIZE"], ["WRITE_SIZE"],
               ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY",
@@ -164,19 +172,189 @@ def pmc_passes(args):
             rows = [row for f in files for row in csv.DictReader(open(f))
                     if "k_render<false" in row.get("Kernel_Name", "")]
             grid = max((int(row.get("Grid_Size", 0) or 0) for row in rows), default=0)
+            rows = [row for row in rows if int(row.get("Grid_Size", 0) or 0) == grid]
+            # not the first launch: it has no previous per-tile costs (supertile order), the timed ones are ordered
+            first = min((int(row["Dispatch_Id"]) for row in rows), default=-1)
+            rows = [row for row in rows if int(row["Dispatch_Id"]) != first]
             agg, cnt = {}, {}
             for row in rows:
-                if int(row.get("Grid_Size", 0) or 0) == grid:
-                    k = row["Counter_Name"]
-                    agg[k] = agg.get(k, 0.0) + float(row["Counter_Value"])
-                    cnt[k] = cnt.get(k, 0) + 1
+                k = row["Counter_Name"]
+                agg[k] = agg.get(k, 0.0) + float(row["Counter_Value"])
+                cnt[k] = cnt.get(k, 0) + 1
             out.update({k: agg[k] / cnt[k] for k in agg})
             out["dispatches"] = max(cnt.values()) if cnt else 0
+            if args.pmc_keep:  # the rows behind these averages, for profiles/ (scripts/reproduce_line.py)
+                kept.extend({"pass": i, "dispatch": int(row["Dispatch_Id"]), "grid": int(row.get("Grid_Size", 0) or 0),
+                             "counter": row["Counter_Name"], "value": float(row["Counter_Value"])} for row in rows)
     except subprocess.TimeoutExpired:
         out.setdefault("error", "PMC pass timed out")
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+    if args.pmc_keep:
+        os.makedirs(args.pmc_keep, exist_ok=True)
+        with open(os.path.join(args.pmc_keep, "bench_pmc.json"), "w") as f:
+            json.dump({"command": child, "passes": passes, "averages": out, "rows": kept}, f, indent=0)
     return out
+
+
+# ------------------------------------------------------------------------------------------------ configs record
+# the other BASELINE configurations in the line the driver runs, one compact record each, measured with
+# the headline's protocol (first frame alone, then W warm-up and K timed frames queued back to back, barrier-free one
+# GPU).  (label, scene config, camera path)
+CONFIG_SET = (("garden", "garden", "static"), ("truck_4k", "truck", "static"), ("lightfield_16", "lightfield", "static"),
+              ("dense", "dense", "static"), ("orbit_0.5deg", "bicycle", "orbit"))
+ORBIT_STEP = 0.5
+
+
+def scene_cached(gv, gen):
+    """The seeded stand-in scene; with GVRT_SCENE_CACHE set, generated once and shared (np.save files) between the
+    configs record's PMC child and the line's own process, which would otherwise both spend ~20 s generating."""
+    d = os.environ.get("GVRT_SCENE_CACHE")
+    if not d:
+        return gv.scene.make(**gen)
+    path = os.path.join(d, f"{gen['kind']}_{gen['n']}_{gen['seed']}.npz")
+    if os.path.exists(path):
+        with np.load(path) as z:
+            return {k: z[k] for k in z.files}
+    sp = gv.scene.make(**gen)
+    tmp = path + f".{os.getpid()}.npz"
+    np.savez(tmp, **sp)
+    os.replace(tmp, path)
+    return sp
+
+
+def config_frames(gv, name, path, nframes):
+    """Per-frame cameras of one configs-record entry: the config camera (config 5: the centred 16-view rig, as
+    `--config lightfield`), or for the orbit path azimuth 30 + k * ORBIT_STEP in frame k."""
+    _, W, H, ncams = gv.scene.CONFIGS[name]
+    views = ncams if name == "lightfield" else 1
+
+    def rig(k):
+        az = 30.0 + (k * ORBIT_STEP if path == "orbit" else 0.0)
+        v, p = gv.camera.lightfield_grid_rig(gv.camera.orbit_eye(4.0, 20.0, az), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0),
+                                             nx=views, ny=1, spacing=0.1, fovy_deg=50.0,
+                                             aspect=gv.camera.aspect_ratio(W, H), centred=name == "lightfield")
+        return np.ascontiguousarray(np.asarray(v, np.float32).reshape(-1)), p
+
+    frames = [rig(k) for k in range(nframes)] if path == "orbit" else [rig(0)] * nframes
+    return frames, W, H, views
+
+
+def run_config_set(gv, torch, steps, warmup, bicycle_r=None, literal=True, bkw=None):
+    """Each CONFIG_SET entry with the headline's timing protocol; returns {label: record} and the number of FAST
+    k_render launches of each entry in launch order (the PMC child's manifest)."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    recs, manifest = {}, []
+    scenes = {}
+    for label, name, path in CONFIG_SET:
+        gen, _, _, _ = gv.scene.CONFIGS[name]
+        key = (gen["kind"], gen["n"], gen["seed"])
+        own = False
+        if key == ("mipnerf", 1_000_000, 1) and bicycle_r is not None:
+            r = bicycle_r
+            m = bicycle_r.m
+        else:
+            if key not in scenes:
+                scenes.clear()
+                scenes[key] = scene_cached(gv, gen)
+            r, own = gv.Renderer(dev.index), True
+            m = r.prepare(scenes[key], **(bkw or {}))
+        nframes = 1 + warmup + steps
+        frames, W, H, views = config_frames(gv, name, path, nframes)
+        params = r.render_params(mode=gv.MODE_FAST)
+        buf = torch.zeros((views * H * W * 4,), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        r.render_device(frames[0][0], frames[0][1], W, H, views, params=params, rgba8_ptr=buf.data_ptr())
+        torch.cuda.synchronize()
+        first_wall = (time.perf_counter() - t) * 1e3
+        first_ms = r.render_ms()
+        for k in range(1, 1 + warmup):
+            r.render_device(frames[k][0], frames[k][1], W, H, views, params=params, rgba8_ptr=buf.data_ptr(),
+                            async_=True)
+        r.sync()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(1 + warmup, nframes):
+            r.render_device(frames[k][0], frames[k][1], W, H, views, params=params, rgba8_ptr=buf.data_ptr(),
+                            async_=True)
+        r.sync()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        kms = float(r.render_ms())
+        rays = W * H * views
+        rec = {"config": f"{name}: {gen['n']} Gaussians ({m} survivors), {W}x{H}" + (f" x {views} views" if views > 1 else "")
+                         + (f", camera orbiting {ORBIT_STEP} deg per frame" if path == "orbit" else ""),
+               "rays_per_step": rays, "kernel_ms": round(kms, 4), "ms_per_step": round(el / steps * 1e3, 4),
+               "mrays": round(rays * steps / el / 1e6, 1), "kernel_mrays": round(rays / (kms * 1e-3) / 1e6, 1),
+               "first_frame_kernel_ms": round(first_ms, 4), "first_frame_wall_ms": round(first_wall, 4)}
+        if path == "static":
+            rec["frame_sha1"] = hashlib.sha1(buf.cpu().numpy().tobytes()).hexdigest()
+        if literal:
+            # SURVEY §8d's algorithmic bytes from the reference algorithm's counters (LITERAL, frame-0 camera)
+            r.set_stats(True)
+            r.render(frames[0][0], frames[0][1], W, H, views, params=r.render_params(mode=gv.MODE_LITERAL),
+                     rgba8=False, rgba32f=False)
+            st = r.stats()
+            r.set_stats(False)
+            b = 48.0 * st["crossings"] + 192.0 * st["accepted"] + 4.0 * rays
+            rec["logical_frac"] = round(b / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            rec["algorithmic_bytes_per_launch"] = b
+        manifest.append([label, nframes])
+        recs[label] = rec
+        del buf
+        if own:
+            r.close()
+    return recs, manifest
+
+
+def configs_pmc(args):
+    """One rocprofv3 SQ pass over a child that renders CONFIG_SET (5 timed + 1 warm-up frames each): the VALU-issue
+    fraction of each entry's ordered launches, attributed by dispatch order (the child's manifest).  Before this
+    process touches the GPU.  Returns {label: {...}} or {"error": ...}."""
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return {"error": "rocprofv3 not found"}
+    steps, warmup = 5, 1
+    child = [sys.executable, os.path.abspath(__file__), "--configs-child", "--steps", str(steps), "--warmup",
+             str(warmup), "--build", args.build]
+    counters = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "GRBM_GUI_ACTIVE"]
+    tmp = tempfile.mkdtemp(prefix="gvrt_cfgpmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        d = os.path.join(tmp, "p")
+        cmd = ["timeout", "-s", "KILL", "240", exe, "--pmc", *counters, "--kernel-include-regex", "k_render",
+               "-d", d, "-o", "run", "--output-format", "csv", "--", *child]
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300,
+                           env=dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp")))
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+        if r.returncode != 0 or not files or not lines:
+            return {"error": f"configs pass: rc {r.returncode} {r.stderr[-300:]}"}
+        manifest = json.loads(lines[-1])["manifest"]
+        per = {}
+        for f in files:
+            for row in csv.DictReader(open(f)):
+                if "k_render<false" in row.get("Kernel_Name", ""):
+                    per.setdefault(int(row["Dispatch_Id"]), {})[row["Counter_Name"]] = float(row["Counter_Value"])
+        ids = sorted(per)
+        need = sum(n for _, n in manifest)
+        if len(ids) != need:
+            return {"error": f"configs pass: {len(ids)} k_render dispatches, manifest {need}"}
+        out, i = {}, 0
+        for label, n in manifest:
+            seg = [per[k] for k in ids[i + n - steps:i + n]]  # the timed (cost-ordered) launches
+            i += n
+            fr = [2.0 * x["SQ_INSTS_VALU"] / (N_SIMD * x["GRBM_GUI_ACTIVE"] / N_XCD) for x in seg]
+            wc = sum(x["SQ_WAVE_CYCLES"] for x in seg)
+            out[label] = {"valu_issue_frac": round(float(np.mean(fr)), 4),
+                          "valu_per_wave": round(sum(x["SQ_INSTS_VALU"] for x in seg) / max(sum(x["SQ_WAVES"] for x in seg), 1), 1),
+                          "wave_cycles": {"issuing": round(sum(x["SQ_ACTIVE_INST_ANY"] for x in seg) / wc, 4),
+                                          "waiting_on_memory": round(sum(x["SQ_WAIT_ANY"] for x in seg) / wc, 4)}}
+        return out
+    except subprocess.TimeoutExpired:
+        return {"error": "configs PMC pass timed out"}
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def tile_cost_calibration(r, vi, pi, W, H, params):
@@ -396,9 +574,25 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1 or (args.exchange and "RANK" in os.environ)
+    if args.configs_child:  # the configs record's PMC child: render CONFIG_SET, print the launch manifest
+        import torch
+        gv = importlib.import_module("3dgvrt_lightfield_amd")
+        bkw = dict(builder=2, collapse=1) if args.build == "quality" else {}
+        _, manifest = run_config_set(gv, torch, args.steps, args.warmup, literal=False, bkw=bkw)
+        print(json.dumps({"manifest": manifest}), flush=True)
+        return
+    with_configs = (not distributed and world == 1 and not args.no_configs and args.config == "bicycle" and not args.ply
+                    and args.camera_path == "static" and args.mode == "fast" and args.split == "views")
+    cache_dir = None
+    if with_configs and not os.environ.get("GVRT_SCENE_CACHE"):
+        cache_dir = tempfile.mkdtemp(prefix="gvrt_scenes_", dir=os.environ.get("TMPDIR", "/tmp"))
+        os.environ["GVRT_SCENE_CACHE"] = cache_dir
     pmc = None
+    cfg_pmc = None
     if not distributed and not args.no_pmc:
         pmc = pmc_passes(args)  # before this process touches the GPU
+        if with_configs:
+            cfg_pmc = configs_pmc(args)
 
     import torch
     import torch.distributed as dist
@@ -553,7 +747,7 @@ def main():
     r.render_device(next_vi(), pi, W, H, ncams, params=params, tiles=tiles, rgba8_ptr=first_buf.data_ptr(),
                     packed=packed)
     torch.cuda.synchronize()
-    first_frame_wall_ms = (time.perf_counter() - t_ff) * 1e3  # includes a probe launch (option probe_order)
+    first_frame_wall_ms = (time.perf_counter() - t_ff) * 1e3  # host call + the unordered launch, synchronous
     first_frame_ms = r.render_ms()
     del first_buf
     for _ in range(args.warmup):
@@ -676,6 +870,12 @@ def main():
                                        "ready_not_issued": round(pmc.get("SQ_WAIT_INST_ANY", 0) / wc, 4)}
         elif logical:  # no PMC passes (--no-pmc or rocprofv3 missing): the logical figure stands in
             roof = {**logical, "traffic": traffic, "note": "no PMC passes: " + str((pmc or {}).get("error", "--no-pmc"))}
+        if roof is not None and traffic is not None and "wave_cycles" in roof:
+            # the binding unit is the busier of the two measured resources: VALU issue or HBM bytes
+            hbm_frac = traffic / (kern_avg * 1e-3) / 1e9 / HBM_PEAK_GBS
+            if hbm_frac > roof["frac"]:
+                roof.update({"bound": "hbm", "achieved": traffic / (kern_avg * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": round(hbm_frac, 4), "valu_issue_frac": roof["frac"]})
         if roof is not None:
             roof["kernel_ms_avg"] = round(kern_avg, 4)
             roof["kernel"] = kern
@@ -774,6 +974,25 @@ def main():
                 vc = None
             balance = rank_balance(args, r, gv, dist_mod, frame_vi[0], pi, W, H, views, params, kern_avg, view_costs=vc)
 
+        # ---- the other BASELINE configurations, after everything else the line measures
+        configs = None
+        if with_configs:
+            t_cfg = time.perf_counter()
+            configs, _ = run_config_set(gv, torch, args.steps, args.warmup, bicycle_r=r, bkw=bkw)
+            for label, rec in configs.items():
+                if cfg_pmc and label in cfg_pmc:
+                    rec.update(cfg_pmc[label])
+                elif cfg_pmc and "error" in cfg_pmc:
+                    rec["valu_issue_frac"] = None
+            configs["_note"] = (f"each config timed as the headline ({args.warmup} warm-up + {args.steps} timed frames "
+                                "queued back to back after an unordered first frame); valu_issue_frac from one rocprofv3 SQ "
+                                "pass of a child rendering the same set (5 timed frames each); logical_frac = SURVEY §8d "
+                                f"bytes / kernel time / 8 TB/s; whole record {time.perf_counter() - t_cfg:.1f} s")
+            if cfg_pmc and "error" in cfg_pmc:
+                configs["_pmc_error"] = cfg_pmc["error"]
+        if cache_dir:
+            shutil.rmtree(cache_dir, ignore_errors=True)
+
         result = {
             "metric": "Mrays/s + fps @1920x1080, 1M Gaussians; PSNR vs Vulkan reference",
             "value": round(mrays, 3),
@@ -825,6 +1044,8 @@ def main():
             result["strong_scaling"] = strong
         if orbit_static:
             result["orbit_same_views_static"] = orbit_static
+        if configs:
+            result["configs"] = configs
         if host_out:
             result["host_output_pcie"] = host_out
         if lit_stats:

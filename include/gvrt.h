@@ -178,8 +178,9 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle h, const gvrt_accel_params* p);
 /* Copy the acceleration structure to host memory (parity checks of the builders, like inspecting a
  * serialized VkAccelerationStructure).  which = 0: the binary tree (n_leaves - 1 nodes of 64 B:
  * child 0 box, child 1 box, c0, c1, split axis, 0); which = 1: the 4-wide tree the render kernel
- * traverses (128 B per node).  *count receives the node count; at most cap nodes are written (out may
- * be NULL to query the count). */
+ * traverses (128 B per node); which = 2: adaptive enclosing only, each leaf's icosahedron half-width
+ * sqrt(3) kernelScale(density) as the build wrote it for the render kernel (4 B per leaf).  *count receives
+ * the element count; at most cap elements are written (out may be NULL to query the count). */
 gvrt_status gvrt_read_accel(gvrt_handle h, int which, void* out, uint64_t cap, uint64_t* count);
 
 /* Particle Rendering pass: buildCommandBuffer (VulkanFullRT.cpp:1185-1244) dispatching

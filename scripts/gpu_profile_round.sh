@@ -11,16 +11,19 @@ mkdir -p $out/pmc
 if [ "$PART" != "2" ]; then
 if [ -z "$PMC_ONLY" ]; then
 if [ -z "$SKIP_TESTS" ]; then
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $out/pytest_gpu.log 2>&1 || { tail -20 $out/pytest_gpu.log; exit 1; }
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $out/pytest_gpu.log 2>&1 || { tail -20 $out/pytest_gpu.log; exit 1; }
 tail -2 $out/pytest_gpu.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || { cat $out/smoke.log; exit 1; }
 tail -1 $out/smoke.log
 fi
-timeout -k 10 400 python bench.py --steps 20 --warmup 3 > $out/bench.json 2> $out/bench.err || { tail -20 $out/bench.err; exit 1; }
+timeout -k 10 500 python bench.py --steps 20 --warmup 5 --pmc-keep $out > $out/bench.json 2> $out/bench.err || { tail -20 $out/bench.err; exit 1; }
 cat $out/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pmc > $out/bench_prof.json 2> $out/bench_prof.err || { tail -20 $out/bench_prof.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-pmc --no-configs > $out/bench_prof.json 2> $out/bench_prof.err || { tail -20 $out/bench_prof.err; exit 1; }
 find $out/prof -name "*kernel_stats.csv" -exec cp {} $out/kernel_stats.csv \;
+find $out/prof -name "*kernel_trace.csv" -exec cp {} $out/kernel_trace.csv \;
 head -5 $out/kernel_stats.csv
+# the line's figures recomputed from the kept PMC rows and the trace's launch groups (first frame / timed / later)
+python3 scripts/reproduce_line.py $out/bench.json $out/bench_pmc.json $out/kernel_trace.csv --warmup 5 --steps 20 > $out/line_reproduction.json && cat $out/line_reproduction.json
 fi
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_DCACHE_REQ SQC_TC_DATA_READ_REQ"; do

@@ -2,8 +2,8 @@
 the driver's 8-GPU node, config 5 with 16 views over 8 ranks).
 
 The renderer is replaced by a deterministic per-pixel pattern so the test checks what the N>1 path
-owns: tile assignment (disjoint, complete), padding of unequal parts for the gather, the gather
-itself and the tile unpack indexing (host mirror of k_unpack)."""
+owns: tile assignment (disjoint, complete), the exact-size point-to-point exchange of unequal parts to
+rank 0 (no padding since round 4), and the tile unpack indexing (host mirror of k_unpack)."""
 import importlib
 import os
 import socket

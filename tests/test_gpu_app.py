@@ -71,7 +71,9 @@ def test_bench_on_a_ply(gv, tmp_path):
     assert line["value"] > 0 and line["roofline"]["frac"] > 0
     # the roofline names its binding unit (instruction issue, from the PMC passes) and is a bound
     roof = line["roofline"]
-    assert roof["bound"] == "issue" and roof["frac"] <= 1.0, roof
+    assert roof["bound"] in ("issue", "hbm") and roof["frac"] <= 1.0, roof
+    # the bound names the busier resource: VALU issue unless the HBM fraction is larger
+    assert (roof["bound"] == "hbm") == (roof["hbm"]["frac"] > roof.get("valu_issue_frac", roof["frac"])), roof
     assert 0.0 < roof["hbm"]["frac"] < 1.0 and roof["logical"]["bound"] == "hbm"
 
 

@@ -1,9 +1,11 @@
 """Full-size SURVEY §8d configurations 3-5 and the dense stand-in on the GPU: size-independent properties plus
-the oracle over the whole frame (garden) or a strided ray sample (the dense stand-in: every 8th ray, 259 k,
-since its ~10 LITERAL rounds of ~150 crossings per ray cost the oracle ~10 min per frame on 16 threads; truck
-4K: every 64th, 130 k rays; the light field: every 64th, 518 k of its 33.2 M rays).  The oracle restates the reference's loop per ray, so a strided sample is a valid
-sample.  Tolerances and the on-threshold accounting as in test_gpu_parity.py (every compared ray is bounded;
-on-threshold fractions capped near their measured values); tile / view splits are checked bit for bit.
+the oracle over every ray of the frame (garden 2.07 M rays, truck 4K 8.29 M, the 16-view light field 33.2 M; round 5,
+VERDICT r04 #1) or, for the dense stand-in, every 4th ray (518 k: its ~10 LITERAL rounds of ~150 crossings per ray
+cost the oracle ~10 min per whole frame on the GPU box's 16 threads).  The oracle restates the reference's loop per
+ray, so a strided sample is a valid sample.  Tolerances and the on-threshold accounting as in test_gpu_parity.py
+(every unflagged ray within 1e-4, every flagged ray within its flip bound); the on-threshold caps sit just above the
+measured fractions (the flags are the CPU oracle's, so the fraction is the same on every box); tile / view splits are
+checked bit for bit.
 
   * config 3 "garden": 3 M Gaussians, 1920x1080
   * config 4 "truck":  2 M Gaussians, 3840x2160, image split in 64x64 blocks over 8 simulated ranks
@@ -50,10 +52,11 @@ def test_garden_3m(gv, O):
     m_ref, sub, ref = _oracle_subset(O, splats, vi, pi, W, H)  # all 2 073 600 rays
     assert m_ref == m
     got = a["rgba32f"].reshape(-1, 4)[sub.astype(np.int64)]
-    _cmp_images(got, ref, amb_max=0.02)
+    _cmp_images(got, ref, amb_max=0.0097)  # measured 0.924 % flagged
     record_parity("garden", **parity_figures(O, gv, got, ref))
 
 
+@pytest.mark.timeout(900)
 def test_truck_4k_tile_split(gv, O):
     """Config 4 split over 8 simulated ranks in both layouts: the 64x64-block round-robin, and the cost bands the
     bench and SplitFrame ship (calibration renders, gvrt_read_tile_costs, dist.band_tiles over
@@ -87,12 +90,14 @@ def test_truck_4k_tile_split(gv, O):
             np.testing.assert_array_equal(frame.cpu().numpy(), full["rgba8"][0], err_msg=name)
         sizes = [len(t) for t in layouts["cost-bands"]]
         assert max(sizes) != min(sizes)  # cost bands: unequal tile counts (equal cost)
-    _, sub, ref = _oracle_subset(O, splats, vi, pi, W, H, stride=64)
-    got = full["rgba32f"].reshape(-1, 4)[sub.astype(np.int64)]
-    _cmp_images(got, ref, amb_max=0.02)
-    record_parity("truck_4k", stride=64, **parity_figures(O, gv, got, ref))
+    _, sub, ref = _oracle_subset(O, splats, vi, pi, W, H)  # all 8 294 400 rays
+    got = full["rgba32f"].reshape(-1, 4)
+    del full
+    _cmp_images(got, ref, amb_max=0.0175)  # 1.61 % flagged on the round-4 1/64 sample
+    record_parity("truck_4k", **parity_figures(O, gv, got, ref))
 
 
+@pytest.mark.timeout(900)
 def test_lightfield_grid_16_views(gv, O):
     splats, W, H, ncams = _scene(gv, "lightfield")
     assert ncams == 16
@@ -110,15 +115,17 @@ def test_lightfield_grid_16_views(gv, O):
     np.testing.assert_allclose(np.linalg.norm(d[..., :3], axis=-1), 1.0, atol=2e-6)
     # neighbouring views see (slightly) different images
     assert np.abs(img[0] - img[15]).max() > 0.01
-    _, sub, ref = _oracle_subset(O, splats, vi, pi, W, H, ncams=ncams, stride=64)
-    got = img.reshape(-1, 4)[sub.astype(np.int64)]
-    _cmp_images(got, ref, amb_max=0.02)
-    record_parity("lightfield_16", stride=64, **parity_figures(O, gv, got, ref))
+    del batch, singles, d
+    _, sub, ref = _oracle_subset(O, splats, vi, pi, W, H, ncams=ncams)  # all 33 177 600 rays
+    got = img.reshape(-1, 4)
+    _cmp_images(got, ref, amb_max=0.017)  # 1.56 % flagged on the round-4 1/64 sample
+    record_parity("lightfield_16", **parity_figures(O, gv, got, ref))
 
 
+@pytest.mark.timeout(900)
 def test_dense_standin(gv, O):
     """The dense stand-in (scene.dense_standin: ~150 crossings, ~79 accepted, ~10 LITERAL rounds per ray):
-    FAST and LITERAL vs the oracle on every 8th ray of the 1080p frame (259 k rays; the oracle's ~10 LITERAL
+    FAST and LITERAL vs the oracle on every 4th ray of the 1080p frame (518 k rays; the oracle's ~10 LITERAL
     rounds of ~150 crossings per ray make the whole frame take ~10 min on the GPU box's 16 threads, too long for
     one test), FAST's accepted-hit counts vs the oracle's on every off-threshold ray."""
     splats, W, H, _ = _scene(gv, "dense")
@@ -127,7 +134,7 @@ def test_dense_standin(gv, O):
         m = r.prepare(splats)
         fast = r.render(vi, pi, W, H, hit_counts=True)
         lit = r.render(vi, pi, W, H, mode=gv.MODE_LITERAL)
-    m_ref, sub, ref = _oracle_subset(O, splats, vi, pi, W, H, stride=8)
+    m_ref, sub, ref = _oracle_subset(O, splats, vi, pi, W, H, stride=4)
     assert m_ref == m
     st = ref["stats"].reshape(-1, 3)
     assert st[:, 0].mean() > 140, st.mean(axis=0)  # the workload is what it claims to be
@@ -135,8 +142,8 @@ def test_dense_standin(gv, O):
     # ~150 crossings and ~10 round boundaries per ray: 7.8 % of the rays carry a decision within the
     # on-threshold margins (measured on a 1/64 sample); each of them is bounded by its flip bound,
     # every other ray must match as everywhere else
-    _cmp_images(fast["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.09)
-    _cmp_images(lit["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.09)
+    _cmp_images(fast["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.082)  # 7.85 % flagged on the 1/8 sample
+    _cmp_images(lit["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.082)
     amb = O.ambiguous(ref["margin"])
     assert (fast["hit_counts"].reshape(-1)[idx] != st[:, 1])[~amb].sum() == 0
-    record_parity("dense", stride=8, **parity_figures(O, gv, fast["rgba32f"].reshape(-1, 4)[idx], ref))
+    record_parity("dense", stride=4, **parity_figures(O, gv, fast["rgba32f"].reshape(-1, 4)[idx], ref))
