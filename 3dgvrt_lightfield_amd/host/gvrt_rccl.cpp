@@ -131,6 +131,48 @@ gvrt_status SplitFrame::rccl(ncclResult_t r, const char* what) {
     return fail(GVRT_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
+gvrt_status SplitFrame::group_failed() {
+    // an RCCL call between ncclGroupStart and ncclGroupEnd failed: close the group, then abort (the peers' matching
+    // calls never complete; their bounded waits time out)
+    (void)ncclGroupEnd();
+    abort_comm();
+    return st_;
+}
+
+gvrt_status SplitFrame::wait(const char* what) {
+    // hipStreamSynchronize would wait forever for a collective whose peer never entered it (a rank that failed before
+    // the call, or aborted its communicator: ncclCommAbort does not notify peers over P2P / SHM links).  Poll the
+    // stream and the communicator's asynchronous error against a deadline instead; a timeout or an error aborts the
+    // communicator, which makes its queued kernels exit.
+    const auto t0 = std::chrono::steady_clock::now();
+    auto sleep = std::chrono::microseconds(20);
+    while (true) {
+        const hipError_t q = hipStreamQuery(stream_);
+        if (q == hipSuccess) return GVRT_OK;
+        if (q != hipErrorNotReady) {
+            fail(GVRT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(q));
+            abort_comm();
+            return st_;
+        }
+        if (comm_) {
+            ncclResult_t ae = ncclSuccess;
+            if (ncclCommGetAsyncError(comm_, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+                fail(GVRT_ERR_RCCL, std::string(what) + ": RCCL async error: " + ncclGetErrorString(ae));
+                abort_comm();
+                return st_;
+            }
+        }
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s_) {
+            fail(GVRT_ERR_RCCL, std::string(what) + ": no progress within " + std::to_string(timeout_s_) +
+                                    " s (a peer did not take part in the exchange)");
+            abort_comm();
+            return st_;
+        }
+        std::this_thread::sleep_for(sleep);
+        sleep = std::min(sleep * 2, std::chrono::microseconds(2000));
+    }
+}
+
 gvrt_status SplitFrame::agree(gvrt_status local) {
     // every rank enters this all-reduce (max of the status magnitudes) before anything rank-specific, so a set-up
     // failure on one rank is every rank's failure and nobody waits in a later collective
@@ -148,8 +190,11 @@ gvrt_status SplitFrame::agree(gvrt_status local) {
         return st_;
     }
     int32_t all = 0;
-    if (hipStreamSynchronize(stream_) != hipSuccess || hipMemcpy(&all, d, sizeof(all), hipMemcpyDeviceToHost) != hipSuccess)
-        s = fail(GVRT_ERR_HIP, "status readback");
+    if (wait("agree") != GVRT_OK) {
+        (void)hipFree(d);
+        return st_;
+    }
+    if (hipMemcpy(&all, d, sizeof(all), hipMemcpyDeviceToHost) != hipSuccess) s = fail(GVRT_ERR_HIP, "status readback");
     (void)hipFree(d);
     if (s == GVRT_OK && all != 0) s = fail((gvrt_status)(-all), local != GVRT_OK ? err_ : "set-up failed on another rank");
     return s == GVRT_OK ? GVRT_OK : st_;
@@ -207,8 +252,7 @@ gvrt_status SplitFrame::cost_classes(std::vector<uint8_t>* classes) {
         return st_;
     }
     std::vector<uint8_t> msg(n + 1, 1);
-    gvrt_status s = GVRT_OK;
-    if (hipStreamSynchronize(stream_) != hipSuccess) s = fail(GVRT_ERR_HIP, "broadcast sync");
+    gvrt_status s = wait("class broadcast");
     if (s == GVRT_OK && hipMemcpy(msg.data(), d, n + 1, hipMemcpyDeviceToHost) != hipSuccess)
         s = fail(GVRT_ERR_HIP, "class readback");
     (void)hipFree(d);
@@ -265,8 +309,7 @@ gvrt_status SplitFrame::view_costs_bcast(std::vector<double>* costs) {
         return st_;
     }
     std::vector<double> msg(nv + 1, 1.0);
-    gvrt_status s = GVRT_OK;
-    if (hipStreamSynchronize(stream_) != hipSuccess) s = fail(GVRT_ERR_HIP, "broadcast sync");
+    gvrt_status s = wait("cost broadcast");
     if (s == GVRT_OK && hipMemcpy(msg.data(), d, sizeof(double) * (nv + 1), hipMemcpyDeviceToHost) != hipSuccess)
         s = fail(GVRT_ERR_HIP, "cost readback");
     (void)hipFree(d);
@@ -344,7 +387,12 @@ SplitFrame::SplitFrame(GvrtApp& app, int rank, int world, const ncclUniqueId& id
 
 SplitFrame::~SplitFrame() {
     (void)hipSetDevice(app_.device.ordinal);
-    if (stream_) (void)hipStreamSynchronize(stream_);
+    if (stream_) {
+        // (bounded: a peer that never entered a queued exchange leaves it pending; the wait then aborts the
+        // communicator, whose kernels exit, and the synchronize below returns)
+        if (comm_) (void)wait("teardown");
+        (void)hipStreamSynchronize(stream_);
+    }
     if (app_.handle() && stream_) (void)gvrt_set_stream(app_.handle(), nullptr);
     for (void* p : d_recv_)
         if (p) (void)hipFree(p);
@@ -382,26 +430,40 @@ gvrt_status SplitFrame::draw(void* frame) {
     if (rs != GVRT_OK) local = fail(GVRT_ERR_HIP, std::string("gvrt_render_async: ") + gvrt_last_error(h));
     // the exchange, entered even after a failed render (the part then holds a stale frame): every rank's part to
     // rank 0 in one group, exact sizes (rank 0 also sends its own part to itself); views land in their frame slots
-    if (rccl(ncclGroupStart(), "ncclGroupStart")) return st_;
+    if (rccl(ncclGroupStart(), "ncclGroupStart")) {
+        abort_comm();
+        return st_;
+    }
     if (layout_ == VIEWS) {
         for (size_t i = 0; i < views_[rank_].size(); ++i)
             if (rccl(ncclSend((uint8_t*)d_part_ + i * view_bytes, view_bytes, ncclUint8, 0, comm_, stream_), "ncclSend"))
-                return st_;
+                return group_failed();
         if (rank_ == 0)
             for (int r = 0; r < world_; ++r)
                 for (uint32_t v : views_[r])
                     if (rccl(ncclRecv((uint8_t*)frame + v * view_bytes, view_bytes, ncclUint8, r, comm_, stream_),
                              "ncclRecv"))
-                        return st_;
+                        return group_failed();
     } else {
-        if (rccl(ncclSend(d_part_, tiles_.size() * 256, ncclUint8, 0, comm_, stream_), "ncclSend")) return st_;
+        if (rccl(ncclSend(d_part_, tiles_.size() * 256, ncclUint8, 0, comm_, stream_), "ncclSend"))
+            return group_failed();
         if (rank_ == 0)
             for (int r = 0; r < world_; ++r)
                 if (rccl(ncclRecv(d_recv_[r], all_tiles_[r].size() * 256, ncclUint8, r, comm_, stream_), "ncclRecv"))
-                    return st_;
+                    return group_failed();
     }
-    if (rccl(ncclGroupEnd(), "ncclGroupEnd")) return st_;
+    if (rccl(ncclGroupEnd(), "ncclGroupEnd")) {
+        abort_comm();
+        return st_;
+    }
     if (local != GVRT_OK) {
+        // this frame's exchange is queued: drain it (bounded) so the peers' matching receives / sends complete, then
+        // abort; a peer that reaches its next exchange learns of it through its own bounded wait
+        const std::string keep = err_;
+        st_ = GVRT_OK;
+        (void)wait("failed frame's exchange");
+        st_ = local;
+        err_ = keep;
         abort_comm();
         return st_;
     }
@@ -419,6 +481,7 @@ gvrt_status SplitFrame::draw(void* frame) {
 
 gvrt_status SplitFrame::sync() {
     if (st_ != GVRT_OK) return st_;
+    if (wait("sync") != GVRT_OK) return st_;  // bounded: the queued frames' exchanges include the peers
     if (gvrt_sync(app_.handle()) != GVRT_OK)
         return fail(GVRT_ERR_HIP, std::string("gvrt_sync: ") + gvrt_last_error(app_.handle()));
     ncclResult_t async_err = ncclSuccess;

@@ -16,11 +16,14 @@
 // rank 0 whole, straight into its slot of the [view][H][W][4] frame.
 //
 // Errors are statuses: an RCCL failure is GVRT_ERR_RCCL (include/gvrt.h), a HIP failure GVRT_ERR_HIP; error()
-// has the text.  No failure leaves a peer waiting in a collective: set-up failures are agreed on by an all-reduce
-// of every rank's status before anything rank-specific, rank 0's calibration result travels with a status word in
-// the one broadcast every rank always enters, and a rank that fails inside draw() still enters that frame's
-// exchange (sending what its part buffer holds) and aborts the communicator before it returns the failure, so the
-// peers' next exchange errors out instead of waiting.
+// has the text.  Failures are made common knowledge where that is possible: set-up failures are agreed on by an
+// all-reduce of every rank's status before anything rank-specific, rank 0's calibration result travels with a status
+// word in the one broadcast every rank always enters, and a rank that fails inside draw() still enters that frame's
+// exchange (sending what its part buffer holds), drains it, and then aborts its communicator.  ncclCommAbort does not
+// notify peers over P2P / SHM links, so every wait on the exchange is bounded instead of trusting that: wait() polls
+// the stream and ncclCommGetAsyncError against a deadline (set_timeout, default 120 s) and aborts the communicator
+// when it passes, so a peer that is gone costs its partners at most the timeout, never a hang.  The multi-rank
+// failure paths are exercised on one rank only (two ranks cannot share one GPU under RCCL).
 #pragma once
 #include <rccl/rccl.h>
 
@@ -70,6 +73,7 @@ class SplitFrame {
     SplitFrame& operator=(const SplitFrame&) = delete;
 
     gvrt_status status() const { return st_; }  // of the constructor (communicator, buffers)
+    void set_timeout(double seconds) { timeout_s_ = seconds; }  // the bound of every wait on the exchange
     const std::string& error() const { return err_; }
 
     // one frame with the app's uniformDataDynamic: this rank's tiles rendered tile-packed, gathered to rank 0 and
@@ -92,7 +96,9 @@ class SplitFrame {
     gvrt_status cost_classes(std::vector<uint8_t>* classes);
     gvrt_status view_costs_bcast(std::vector<double>* costs);
     gvrt_status agree(gvrt_status local);  // every rank's set-up status, all-reduced: the worst one everywhere
-    void abort_comm();                     // a failure inside draw(): peers' next exchange errors out
+    void abort_comm();                     // ncclCommAbort: this rank's queued RCCL kernels exit
+    gvrt_status group_failed();            // an RCCL call inside a group failed: end the group, abort
+    gvrt_status wait(const char* what);    // the stream, bounded by timeout_s_ and watching RCCL's async error
 
     GvrtApp& app_;
     int rank_, world_;
@@ -100,6 +106,7 @@ class SplitFrame {
     gvrt_status st_ = GVRT_OK;
     std::string err_;
     ncclComm_t comm_ = nullptr;
+    double timeout_s_ = 120.0;
     hipStream_t stream_ = nullptr;
     std::vector<gvrt_tile> tiles_;                  // this rank's tile list
     std::vector<std::vector<gvrt_tile>> all_tiles_;  // every rank's (rank 0 scatters with them)

@@ -92,6 +92,9 @@ def parse():
     ap.add_argument("--configs-child", action="store_true", help=argparse.SUPPRESS)  # PMC child of the configs record
     ap.add_argument("--pmc-keep", default=None, metavar="DIR",
                     help="keep the per-dispatch PMC rows of the line's own passes as DIR/bench_pmc.json (profiles/)")
+    ap.add_argument("--strong-budget-s", type=float, default=300.0,
+                    help="N-rank runs: a strong-scaling sub-record starts only while the run's wall time is below this "
+                         "(rank 0 decides, every rank follows); later ones are listed as skipped, so the line still prints")
     ap.add_argument("--build", default="quality", choices=["quality", "fast"],
                     help="quality: device binned-SAH tree + SAH-optimal 4-wide collapse (the static-scene build, "
                          "as the reference's PREFER_FAST_TRACE BLAS); fast: device LBVH + greedy collapse")
@@ -564,6 +567,9 @@ def rank_balance(args, r, gv, dist_mod, vi_all, pi, W, H, views, params, full_ms
             "note": "each part alone on one GPU with its own cost-ordered dispatch; median of the ordered launches"}
 
 
+T_START = time.perf_counter()
+
+
 def main():
     args = parse()
     dist_mod = importlib.import_module("3dgvrt_lightfield_amd.dist")  # no GPU work at import
@@ -802,6 +808,16 @@ def main():
     strong = []
     if distributed and args.strong != "none":
         for name in [x for x in args.strong.split(",") if x]:
+            # the wall-time budget: rank 0's clock decides for every rank (one broadcast), so no rank waits in a
+            # sub-record its peers skipped
+            go = torch.tensor([1.0 if time.perf_counter() - T_START < args.strong_budget_s else 0.0], device=dev)
+            dist.broadcast(go, src=0)
+            if go.item() == 0.0:
+                if rank == 0:
+                    strong.append({"frame": name, "skipped": f"wall-time budget {args.strong_budget_s:.0f} s reached "
+                                                              f"({time.perf_counter() - T_START:.0f} s into the run)"})
+                continue
+            t_rec = time.perf_counter()
             if name == "bicycle" and args.config == "bicycle" and not args.ply:
                 rs, own = r, False
             else:
@@ -817,6 +833,7 @@ def main():
             if own:
                 rs.close()
             if rec:
+                rec["wall_s"] = round(time.perf_counter() - t_rec, 2)  # scene build, calibration and the timed frames
                 strong.append(rec)
 
     if rank == 0:

@@ -91,7 +91,15 @@ def _exchange_worker(rank, world, port, split, width, height, views, nframes, q)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     d = importlib.import_module("3dgvrt_lightfield_amd.dist")
     counter = [0]
-    if split == "tiles":
+    if split == "bands":
+        # the cost-band layout bench.py and SplitFrame ship: contiguous runs of equal cost over a seeded class map
+        # (rank 0's calibration broadcasts one; every rank cuts the same bands)
+        ty_n, tx_n = (height + 7) // 8, (width + 7) // 8
+        classes = np.random.default_rng(5).integers(0, 40, (1, ty_n, tx_n)).astype(np.uint8)
+        all_tiles = d.band_tiles(width, height, world, costs=d.cost_weights(classes), block=2)
+        sizes, item = [t.shape[0] * 64 for t in all_tiles], (4,)
+        split = "tiles"
+    elif split == "tiles":
         all_tiles = d.rank_tiles(width, height, 1, world, block=2)
         sizes, item = [t.shape[0] * 64 for t in all_tiles], (4,)
     else:
@@ -141,7 +149,8 @@ def _exchange_worker(rank, world, port, split, width, height, views, nframes, q)
 
 @pytest.mark.parametrize("world,split,width,height,views", [(2, "tiles", 100, 60, 1), (3, "tiles", 37, 29, 1),
                                                              (2, "views", 24, 16, 5), (3, "views", 16, 8, 3),
-                                                             (8, "tiles", 72, 40, 1), (8, "views", 16, 8, 16)])
+                                                             (8, "tiles", 72, 40, 1), (8, "views", 16, 8, 16),
+                                                             (8, "bands", 200, 120, 1)])
 def test_frame_exchange_double_buffered(world, split, width, height, views):
     """bench.py's N-rank path on CPU: dist.FrameExchange with two send buffers in flight, unequal parts (tiles:
     ragged block counts; views: 5 views over 2 ranks) sent point to point at their exact sizes (no padding: every
@@ -165,7 +174,7 @@ def test_frame_exchange_double_buffered(world, split, width, height, views):
         np.testing.assert_array_equal(got[k], frame_pattern(k, width, height, views))
     assert res["marks"] == ["rendered", "posted", "exchanged", "assembled"]
     sizes = res["sizes"]
-    item = 4 if split == "tiles" else height * width * 4
+    item = 4 if split in ("tiles", "bands") else height * width * 4
     assert res["send_shape"][0] == sizes[0]
     assert res["exchange_bytes"] == sum(sizes[1:]) * item  # exact parts: no padding on the wire
     assert res["padded"] == (world - 1) * max(sizes) * item

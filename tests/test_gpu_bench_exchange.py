@@ -15,7 +15,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-COMMON = ["--gpus", "1", "--steps", "3", "--warmup", "1", "--no-pmc", "--no-cpu-baseline", "--no-stats"]
+COMMON = ["--gpus", "1", "--steps", "3", "--warmup", "1", "--no-pmc", "--no-cpu-baseline", "--no-stats", "--no-configs"]
 
 
 def _bench(args, distributed):
@@ -56,3 +56,15 @@ def test_bench_exchange_step_matches_single_gpu(split, strong):
         assert len(r["kernel_ms_per_rank"]) == len(r["exchange_ms_per_rank"]) == 1 and r["kernel_ms_per_rank"][0] > 0
         assert r["exchange_bytes"] == 0 and r["bytes_sent_per_rank"][0] == r["tiles_per_rank"][0] * 256
         assert r["one_gpu_kernel_ms"] > 0 and r["assemble_ms"] >= 0
+        assert r["wall_s"] > 0  # each sub-record reports its own wall time
+
+
+def test_bench_exchange_strong_budget_prints_partial_line():
+    """A strong-scaling sub-record starts only within the run's wall-time budget (--strong-budget-s): past it the
+    line still prints, the records listed as skipped (an 8-rank run must not run past the driver's
+    timeout for lack of a line)."""
+    ex = _bench(["--config", "bicycle", "--split", "views", "--strong", "bicycle,truck", "--strong-budget-s", "0"],
+                distributed=True)
+    assert ex["value"] > 0
+    assert [r["frame"] for r in ex["strong_scaling"]] == ["bicycle", "truck"]
+    assert all("skipped" in r for r in ex["strong_scaling"])
