@@ -36,7 +36,7 @@ STATUS_NAMES = {
 # per-handle tuning switches (gvrt_set_option; include/gvrt.h GVRT_OPT_*)
 OPTIONS = {"tile_order": 0, "tile_xcd": 1, "octant_nodes": 2, "record_origins": 3, "box_slack": 4,
            "packed_kbuffer": 5, "order_spread": 6,
-           "accept_boxes": 7, "optional_mem_mb": 8, "compact_nodes": 9}
+           "accept_boxes": 7, "optional_mem_mb": 8}
 MODE_FAST = 0
 MODE_LITERAL = 1
 

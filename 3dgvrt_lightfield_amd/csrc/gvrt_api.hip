@@ -270,26 +270,11 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
     gvrt_dfree(c, (void**)&c->d_nodes4x8);
     gvrt_dfree(c, (void**)&c->d_nodes4e);
     gvrt_dfree(c, (void**)&c->d_nodes4ex8);
-    gvrt_dfree(c, (void**)&c->d_c4);
-    gvrt_dfree(c, (void**)&c->d_c4e);
     c->accept_ok = false;
     c->accept_nomem = false;
     gvrt_status s = gvrt_launch_build_accel(c, *p);
     if (s) return s;
-    // the build's tail, timed into accel_ms: leaf ids consecutive per node, the octant copies, the compact nodes
-    GVRT_HIP(c, hipEventRecord(c->ev0, c->stream));
-    if ((s = gvrt_renumber_leaves(c))) {
-        c->accel = false;
-        return s;
-    }
     if ((s = gvrt_launch_node_octants(c))) return s;
-    if ((s = gvrt_launch_compact_nodes(c, c->d_nodes4, &c->d_c4))) return s;
-    GVRT_HIP(c, hipEventRecord(c->ev1, c->stream));
-    GVRT_HIP(c, hipEventSynchronize(c->ev1));
-    {
-        float ms = 0.0f;
-        if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->stats.accel_ms += ms;
-    }
     // adaptive enclosing: each leaf's icosahedron half-width, a required array allocated with the build (a render
     // never allocates it, so a handle that builds also renders without a new out-of-memory point)
     if ((c->enc.opts & 1u) && c->n_leaves) {
@@ -718,14 +703,6 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         if (c->accept_ok) {
             a.nodes = c->d_nodes4e;
             a.nodes8 = c->opt[GVRT_OPT_OCTANT_NODES] ? c->d_nodes4ex8 : nullptr;
-        }
-    }
-    // the compact 64-B copies of the node set just chosen (the FAST K = 24 kernels read them; others ignore them)
-    {
-        const Bvh4C* cn = a.nodes == c->d_nodes4e ? c->d_c4e : (a.nodes == c->d_nodes4 ? c->d_c4 : nullptr);
-        if (c->opt[GVRT_OPT_COMPACT_NODES] && cn && p->mode == GVRT_MODE_FAST) {
-            a.cnodes = cn;
-            a.cnodes8 = c->opt[GVRT_OPT_OCTANT_NODES] ? cn + c->n_nodes4 : nullptr;
         }
     }
     // Single-origin FAST launches at the default depth read each leaf's kernel-frame origin ok from its record:

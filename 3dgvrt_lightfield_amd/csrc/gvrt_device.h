@@ -58,21 +58,6 @@ struct alignas(16) Bvh4Node {  // (name kept from the 4-wide layout; BVH_W child
 };
 static_assert(sizeof(Bvh4Node) == 28 * BVH_W + 16, "node layout: 128 B (4-wide) / 240 B (8-wide)");
 
-// Compact 4-wide node (64 B: one s_load_dwordx16 per visit, 16 SGPRs), built from a Bvh4Node array by
-// gvrt_launch_compact_nodes for the FAST render kernel.  Child boxes are f16 offsets from an f16 node origin, rounded
-// outward (the decoded box contains the f32 one: culling stays conservative); a plane is consumed straight from its
-// SGPR half by v_fma_mix_f32, t = h * (1/d) + (O - o) * (1/d).  Child links are two bases: a node's inner children
-// are consecutive node ids (breadth-first collapse) and, after the build's leaf renumbering, its leaf children are
-// consecutive leaf ids, each in slot order.  Empty (and dropped) slots hold +inf planes, which no ray can hit.
-struct alignas(16) Bvh4C {
-    uint32_t plane[12];  // child k, axis a at 3k + a: lo | hi << 16 (f16); octant copies: near | far << 16
-    uint32_t oxy;        // node origin x | y << 16 (f16, <= every child's lo)
-    uint32_t ozm;        // origin z | meta << 16: meta bits 0-3 inner-child slots, 4-7 leaf slots, 8-9 split axis
-    uint32_t ibase;      // node id of the first inner child; an all-leaf node: its acceptance widening D (f32 bits)
-    uint32_t lbase;      // leaf id of the first leaf child
-};
-static_assert(sizeof(Bvh4C) == 64, "compact node: 64 B");
-constexpr uint32_t F16_INF2 = 0x7C007C00u;  // both planes +inf: an empty slot
 
 struct f3 {
     float x, y, z;
@@ -123,8 +108,6 @@ struct RenderArgs {
     const Bvh4Node* nodes8;  // the 4-wide nodes in 8 copies, copy o with each axis a of o's bits stored (hi, lo):
     uint64_t nodes8_stride;  // a wave whose rays share octant o reads (near, far) planes in place (nodes per copy)
     uint32_t box_exact;  // box padding covers the plane rounding for these cameras: no per-child slack
-    const Bvh4C* cnodes;   // compact 64-B nodes for the FAST K = 24 kernel (copy 0), or null: the 128-B nodes
-    const Bvh4C* cnodes8;  // their 8 octant copies (cnodes + nodes8_stride x (1 + o)), or null
     float grid_min[3];  // split grid (SplitBLAS analogue): origin and 1 / cell size
     float grid_inv;
     uint8_t* rgba8;

@@ -57,11 +57,6 @@ struct gvrt_context {
     // copies, for the acceptance thresholds in accept_key (refit when a launch brings other thresholds)
     gvrt::Bvh4Node* d_nodes4e = nullptr;
     gvrt::Bvh4Node* d_nodes4ex8 = nullptr;
-    // compact 64-B nodes (gvrt_nodes.hip) for the FAST K = 24 kernel: copy 0 plain, copies 1..8 the octant copies;
-    // d_c4 from the proxy-box nodes (per build), d_c4e from the acceptance nodes (per acceptance refit); null when
-    // they did not fit or a box exceeds the f16 range (the kernel then reads the 128-B nodes)
-    gvrt::Bvh4C* d_c4 = nullptr;
-    gvrt::Bvh4C* d_c4e = nullptr;
     float accept_key[2] = {0.0f, 0.0f};
     bool accept_ok = false;
     bool accept_nomem = false;  // the acceptance copy did not fit (until the next build)
@@ -149,7 +144,7 @@ struct gvrt_context {
 
     gvrt_stats stats{};
     // per-handle tuning switches (gvrt_set_option), measured-best defaults
-    int64_t opt[GVRT_OPT_COUNT] = {1, 1, 1, 1, 0, 1, 0, 1, 0, 1};
+    int64_t opt[GVRT_OPT_COUNT] = {1, 1, 1, 1, 0, 1, 0, 1, 0};
 };
 
 gvrt_status gvrt_fail(gvrt_context* c, gvrt_status code, const std::string& msg);
@@ -176,11 +171,6 @@ gvrt_status gvrt_ploc_build(gvrt_context* c, uint32_t m, const float* leaf_boxes
 // gvrt_sah.hip (the quality build on the device: binned SAH + SAH-optimal collapse)
 gvrt_status gvrt_sah_build_device(gvrt_context* c, uint64_t m, const float* lboxes, gvrt::BvhNode* nodes,
                                   gvrt::Bvh4Node* out4, uint32_t* depth_out, uint64_t* n4_out, uint32_t* depth4_out);
-// gvrt_nodes.hip: leaf ids renumbered so that each node's leaf children are consecutive (per-leaf arrays and the
-// binary tree follow), once per build; the compact copies (9 x n_nodes4) of src into *dst, or *dst = null when they
-// do not fit or a box exceeds the f16 range
-gvrt_status gvrt_renumber_leaves(gvrt_context* c);
-gvrt_status gvrt_launch_compact_nodes(gvrt_context* c, const gvrt::Bvh4Node* src, gvrt::Bvh4C** dst);
 // gvrt_render.hip
 // the render launch; ev_start / ev_stop are recorded at the kernel's start and end (its kernel time)
 gvrt_status gvrt_launch_render_mode(gvrt_context* c, const gvrt::RenderArgs& a, uint64_t nwaves, bool literal,

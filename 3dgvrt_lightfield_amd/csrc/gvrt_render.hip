@@ -361,42 +361,6 @@ __device__ inline RenderRec load_rec_hk_at(const RenderRec* __restrict__ base, c
     hk = h;
     return __builtin_bit_cast(RenderRec, v);
 }
-// Compact node (Bvh4C, 64 B): one s_load_dwordx16 and one wait per visit
-__device__ inline sv16 load_cnode_at(const Bvh4C* __restrict__ base, int32_t idx) {
-    sv16 v;
-    const uint32_t off = (uint32_t)idx << 6;
-    asm volatile("s_load_dwordx16 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(base), "s"(off));
-    return v;
-}
-// fma(f16 half of an SGPR word, b, c) in one v_fma_mix_f32: the node's planes are read straight from the scalar-loaded
-// node (op_sel picks the half; the f16 converts exactly, one f32 rounding).  NEG: fma(h, b, -c)
-template <bool HI, bool NEG = false>
-__device__ inline float fmix(int32_t w, float b, float c) {
-    float r;
-    if constexpr (HI && NEG) asm("v_fma_mix_f32 %0, %1, %2, -%3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "s"(w), "v"(b), "v"(c));
-    else if constexpr (HI) asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "s"(w), "v"(b), "v"(c));
-    else if constexpr (NEG) asm("v_fma_mix_f32 %0, %1, %2, -%3 op_sel_hi:[1,0,0]" : "=v"(r) : "s"(w), "v"(b), "v"(c));
-    else asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "s"(w), "v"(b), "v"(c));
-    return r;
-}
-// Slab test of compact child k: planes t = h * inv + c, c = (O - o) * inv per axis (the node's origin term).  OCT: the
-// octant copy's (near, far) halves, no min / max pairs (as box_hit_nf); else (lo, hi) halves sorted per axis (box_hit)
-template <bool SLACK, bool OCT>
-__device__ inline bool box_hit_c(int32_t wx, int32_t wy, int32_t wz, f3 inv, f3 cc, float t0, float t1) {
-    const float ax = fmix<false>(wx, inv.x, cc.x), bx = fmix<true>(wx, inv.x, cc.x);
-    const float ay = fmix<false>(wy, inv.y, cc.y), by = fmix<true>(wy, inv.y, cc.y);
-    const float az = fmix<false>(wz, inv.z, cc.z), bz = fmix<true>(wz, inv.z, cc.z);
-    float tn, tf;
-    if constexpr (OCT) {
-        tn = fmaxf(fmaxf(t0, ax), fmaxf(ay, az));
-        tf = fminf(fminf(t1, bx), fminf(by, bz));
-    } else {
-        tn = fmaxf(fmaxf(t0, fminf(ax, bx)), fmaxf(fminf(ay, by), fminf(az, bz)));
-        tf = fminf(fminf(t1, fmaxf(ax, bx)), fminf(fmaxf(ay, by), fmaxf(az, bz)));
-    }
-    if constexpr (SLACK) return tn <= tf + 2e-6f * fabsf(tf);
-    else return tn <= tf;
-}
 #define NODE_BOX(nd, k, j) (nd).f(6 * (k) + (j))
 #define NODE_CHILD(nd, k) (nd).w(24 + (k))
 #define NODE_PAD(nd, j) (nd).w(29 + (j))
@@ -527,10 +491,8 @@ _Pragma("unroll")                                                               
 constexpr uint32_t ST_W = 8, ST_H = 4;
 constexpr int RENDER_MIN_WAVES = 4;
 
-template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK, bool SLACK, bool OKREC, bool OKCAM = false,
-          bool NODEC = false>
+template <bool LITERAL, bool ADAPTIVE, int KB, bool STATS, bool PACK, bool SLACK, bool OKREC, bool OKCAM = false>
 __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArgs a, const Bvh4Node* __restrict__ nodes_,
-                                                                 const Bvh4C* __restrict__ cnodes_,
                                                                  const RenderRec* __restrict__ recs_,
                                                                  const RenderRec* __restrict__ crecs_,
                                                                  const uint4* __restrict__ aux_,
@@ -666,16 +628,12 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
     // changes sign) read the plain nodes
     bool octw = false;
     const Bvh4Node* __restrict__ nbase = nodes_;
-    const Bvh4C* __restrict__ cbase = cnodes_;  // NODEC: the compact copies (copy 0 plain, 1 + o octant o)
-    if (NODEC ? a.cnodes8 != nullptr : a.nodes8 != nullptr) {
+    if (a.nodes8) {
         const uint32_t oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
         const uint64_t am = __builtin_amdgcn_ballot_w64(active);
         const uint32_t oct0 = (uint32_t)__builtin_amdgcn_readlane((int)oct, am ? (int)__builtin_ctzll(am) : 0);
         octw = __builtin_amdgcn_ballot_w64(active && oct != oct0) == 0;
-        if (octw) {
-            if constexpr (NODEC) cbase = a.cnodes8 + a.nodes8_stride * oct0;
-            else nbase = a.nodes8 + a.nodes8_stride * oct0;
-        }
+        if (octw) nbase = a.nodes8 + a.nodes8_stride * oct0;
     }
 
     static_assert(!(LITERAL && PACK), "LITERAL keeps rejected crossings: unpacked k-buffer");
@@ -751,42 +709,9 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                 wadd(W_LATE, s_wst[W_ROUNDS] > 1 ? 1u : 0u);
                 s_tph[0] = __builtin_amdgcn_s_memtime();  // the node phase includes the fetch
             }
+            const NodeS nd = load_node_at(nbase, unii(cur));  // whole node: 2x s_load_dwordx16
             float tc = fminf(fminf(thi, kt[KB - 1]), tcut);
             float tl = tlo;
-            uint64_t bal[BVH_W];
-            int32_t ch[BVH_W];
-            uint32_t inner, axis;
-            uint32_t lslots = 0, cib = 0, clb = 0;  // NODEC: leaf slots, first inner / leaf child ids
-            if constexpr (NODEC) {
-                const sv16 cn = load_cnode_at(cbase, unii(cur));  // whole node: one s_load_dwordx16
-                const uint32_t meta = (uint32_t)cn[13] >> 16;
-                inner = meta & 15u;
-                lslots = (meta >> 4) & 15u;
-                axis = (meta >> 8) & 3u;
-                cib = (uint32_t)cn[14];
-                clb = (uint32_t)cn[15];
-                // acceptance widening D: all-leaf nodes of the acceptance copy carry it in place of the inner base
-                const float dn = inner == 0u ? __int_as_float((int32_t)cib) : 0.0f;
-                tl = tlo - dn;
-                tc = tc + dn;
-                // per axis (O - o) / d: the node origin's part of every plane of the node (3 VALU per visit)
-                const f3 cc = mk3(fmix<false, true>(cn[12], inv.x, oinv.x), fmix<true, true>(cn[12], inv.y, oinv.y),
-                                  fmix<false, true>(cn[13], inv.z, oinv.z));
-                if (octw) {
-                    f3 iv = inv;
-                    asm("" : "+v"(iv.x), "+v"(iv.y), "+v"(iv.z));
-#pragma unroll
-                    for (int k = 0; k < BVH_W; ++k)
-                        bal[k] = __builtin_amdgcn_ballot_w64(
-                            box_hit_c<SLACK, true>(cn[3 * k], cn[3 * k + 1], cn[3 * k + 2], iv, cc, tl, tc));
-                } else {
-#pragma unroll
-                    for (int k = 0; k < BVH_W; ++k)
-                        bal[k] = __builtin_amdgcn_ballot_w64(
-                            box_hit_c<SLACK, false>(cn[3 * k], cn[3 * k + 1], cn[3 * k + 2], inv, cc, tl, tc));
-                }
-            } else {
-            const NodeS nd = load_node_at(nbase, unii(cur));  // whole node: 2x s_load_dwordx16
             if constexpr (PACK) {
                 // acceptance-box nodes (FAST): the leaf children's boxes bound each particle's acceptance ellipsoid,
                 // which lies within the node's D (pad[2]) of an admitted crossing along the ray, so the range is
@@ -795,6 +720,7 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                 tl = tlo - dn;
                 tc = tc + dn;
             }
+            uint64_t bal[BVH_W];
             if (octw) {
                 // (an opaque copy of 1/d: otherwise the first child's plane FMAs, common to both tests, are hoisted
                 // above the branch and every min / max input after it gets a canonicalising v_max)
@@ -812,14 +738,9 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                         box_hit<SLACK>(NODE_BOX(nd, k, 0), NODE_BOX(nd, k, 2), NODE_BOX(nd, k, 4), NODE_BOX(nd, k, 1),
                                        NODE_BOX(nd, k, 3), NODE_BOX(nd, k, 5), oinv, inv, tl, tc));
             }
+            int32_t ch[BVH_W];
 #pragma unroll
             for (int k = 0; k < BVH_W; ++k) ch[k] = unii(NODE_CHILD(nd, k));
-            inner = uni(NODE_PAD(nd, 1));
-            axis = uni(NODE_PAD(nd, 0));
-            }
-            // child ids: the 128-B node's links, or (NODEC) consecutive ids from the node's two bases
-#define CHILD_INNER(k) (NODEC ? (int32_t)(cib + (uint32_t)__builtin_popcount(inner & ((1u << (k)) - 1u))) : GVRT_PICK(ch, k))
-#define CHILD_LEAF(k) (NODEC ? (int32_t)(clb + (uint32_t)__builtin_popcount(lslots & ((1u << (k)) - 1u))) : ~GVRT_PICK(ch, k))
             // ---- children in the node's stored order (in-order of the binary split), forward when the
             // first lane's ray points along +axis, else backward: a handful of SALU ops per node
             // (sorting the hit children by the first hitting lane's entry distance cost ~100 SALU per node and
@@ -828,17 +749,18 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
 #pragma unroll
             for (int k = 0; k < BVH_W; ++k) hm |= nz_bit(bal[k], 1u << k);
             if constexpr (STATS) wadd(W_DEAD, hm == 0 ? 1u : 0u);
+            const uint32_t inner = uni(NODE_PAD(nd, 1));
             uint32_t leafmask = hm & ~inner;
             uint32_t im = hm & inner;
             int32_t next = -1;
             if (im) {
-                const bool rev = (rsign >> axis) & 1u;
+                const bool rev = (rsign >> uni(NODE_PAD(nd, 0))) & 1u;
                 const int first = rev ? 31 - __clz(im) : __ffs(im) - 1;
-                next = CHILD_INNER(first);
+                next = GVRT_PICK(ch, first);
                 im &= ~(1u << first);
                 while (im) {  // the next child in visiting order ends on top
                     const int k = rev ? __ffs(im) - 1 : 31 - __clz(im);
-                    push(CHILD_INNER(k));
+                    push(GVRT_PICK(ch, k));
                     im &= ~(1u << k);
                 }
             } else if (sp > 0) {
@@ -854,10 +776,8 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
             while (leafmask) {
                 const int k = __builtin_ctz(leafmask);
                 leafmask &= leafmask - 1;
-                GVRT_LEAF(CHILD_LEAF(k), GVRT_PICK(bal, k))  // leaf slot, lanes whose ray hits its box
+                GVRT_LEAF(~GVRT_PICK(ch, k), GVRT_PICK(bal, k))  // leaf slot, lanes whose ray hits its box
             }
-#undef CHILD_INNER
-#undef CHILD_LEAF
             if constexpr (STATS) wadd(C_LEAF, __builtin_amdgcn_s_memtime() - s_tph[1]);
             if (next < 0) break;
             cur = next;  // uniform by construction; readfirstlane at the load lets the compiler see it
@@ -1067,24 +987,17 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
     const dim3 g((unsigned)blocks), b(64);
     // every pointer is its own __restrict__ argument: the uniform node / record loads can then be
     // proven unclobbered by the output stores and are emitted as scalar (s_load) loads
-#define KARGS a.nodes, a.cnodes, a.recs, a.crecs, a.aux, a.sh, a.view_inv, a.tiles, a.rgba8, a.rgba32f, a.ray_dirs, \
-              a.hit_counts, a.stats
+#define KARGS a.nodes, a.recs, a.crecs, a.aux, a.sh, a.view_inv, a.tiles, a.rgba8, a.rgba32f, a.ray_dirs, a.hit_counts, a.stats
     // the kernel-time events ride on the dispatch itself (hipExtLaunchKernelGGL): no separate event packets
     // between one frame's render and the next launch
-#define GVRT_LAUNCH_SOCN(L, A, K, P, S, O, C, N)                                                                \
-    do {                                                                                                        \
-        if (a.stats)                                                                                            \
-            hipExtLaunchKernelGGL((k_render<L, A, K, true, P, S, O, C, N>), g, b, 0, c->stream, ev_start, ev_stop, \
-                                  0u, a, KARGS);                                                                \
-        else                                                                                                    \
-            hipExtLaunchKernelGGL((k_render<L, A, K, false, P, S, O, C, N>), g, b, 0, c->stream, ev_start, ev_stop, \
-                                  0u, a, KARGS);                                                                \
-    } while (0)
-    // the default FAST depth traverses the compact 64-B nodes when render_impl found them (RenderArgs::cnodes)
 #define GVRT_LAUNCH_SOC(L, A, K, P, S, O, C)                                                                    \
     do {                                                                                                        \
-        if (a.cnodes) GVRT_LAUNCH_SOCN(L, A, K, P, S, O, C, (K == K_FAST_DEFAULT && P && !L && !A));            \
-        else GVRT_LAUNCH_SOCN(L, A, K, P, S, O, C, false);                                                      \
+        if (a.stats)                                                                                            \
+            hipExtLaunchKernelGGL((k_render<L, A, K, true, P, S, O, C>), g, b, 0, c->stream, ev_start, ev_stop, 0u, \
+                                  a, KARGS);                                                                    \
+        else                                                                                                    \
+            hipExtLaunchKernelGGL((k_render<L, A, K, false, P, S, O, C>), g, b, 0, c->stream, ev_start, ev_stop,   \
+                                  0u, a, KARGS);                                                                \
     } while (0)
 #define GVRT_LAUNCH_SO(L, A, K, P, S, O) GVRT_LAUNCH_SOC(L, A, K, P, S, O, false)
 #define GVRT_LAUNCH(L, A, K, P) GVRT_LAUNCH_SO(L, A, K, P, true, false)
@@ -1131,7 +1044,6 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
 #undef GVRT_LAUNCH_F
 #undef GVRT_LAUNCH_SO
 #undef GVRT_LAUNCH_SOC
-#undef GVRT_LAUNCH_SOCN
 #undef KARGS
     GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;
@@ -1472,8 +1384,6 @@ gvrt_status gvrt_launch_accept_nodes(gvrt_context* c, float min_response, float 
         hipLaunchKernelGGL(k_node_octants, dim3((unsigned)((8 * n + 255) / 256)), dim3(256), 0, c->stream, n,
                            c->d_nodes4e, c->d_nodes4ex8);
     GVRT_HIP(c, hipGetLastError());
-    gvrt_status s = gvrt_launch_compact_nodes(c, c->d_nodes4e, &c->d_c4e);
-    if (s) return s;
     c->accept_key[0] = min_response;
     c->accept_key[1] = alpha_min;
     c->accept_ok = true;

@@ -271,10 +271,7 @@ gvrt_status gvrt_get_device_buffers(gvrt_handle h, gvrt_device_buffers* out);
                                        acceptance node copies, record-origin copies) are allocated only while the
                                        handle's device memory stays within N MiB; a copy that does not fit (or
                                        whose hipMalloc fails) is left out and launches run without it */
-#define GVRT_OPT_COMPACT_NODES 9u  /* 1 (default): the FAST k-buffer kernel traverses 64-B nodes (f16 child planes
-                                       relative to an f16 node origin, rounded outward; one scalar load per visit);
-                                       0: the 128-B f32 nodes.  Scenes whose boxes exceed the f16 range keep 128 B */
-#define GVRT_OPT_COUNT 10u
+#define GVRT_OPT_COUNT 9u
 gvrt_status gvrt_set_option(gvrt_handle h, uint32_t option, int64_t value);
 gvrt_status gvrt_get_option(gvrt_handle h, uint32_t option, int64_t* value);
 

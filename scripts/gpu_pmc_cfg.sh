@@ -1,8 +1,8 @@
-# Cache-counter passes on one config's render loop: GVRT_CFG=dense bash scripts/gpu_pmc_cfg.sh
+# Cache-counter passes on one config's render loop: GVRT_CFG=dense [GVRT_OPTS=compact_nodes=1 GVRT_TAG=c1] bash scripts/gpu_pmc_cfg.sh
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-out=gpurun_out/pmc_${GVRT_CFG:-bicycle}
+out=gpurun_out/pmc_${GVRT_CFG:-bicycle}${GVRT_TAG:+_$GVRT_TAG}
 mkdir -p $out
 i=0
 for set in "TCC_HIT_sum TCC_MISS_sum" "SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_DCACHE_REQ SQC_TC_DATA_READ_REQ" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "FETCH_SIZE"; do

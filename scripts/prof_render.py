@@ -8,7 +8,10 @@ k = int(os.environ.get("GVRT_K", "0"))
 gen, W, H, _ = gv.scene.CONFIGS[cfg]
 s = gv.scene.make(**gen)
 vi, pi = (gv.scene.mipnerf_camera(W, H) if cfg != "config1" else gv.scene.config1_camera(W, H))
+opts = [kv.split("=") for kv in os.environ.get("GVRT_OPTS", "").split(",") if kv]
 with gv.Renderer(0) as r:
+    for name, val in opts:  # per-handle options (same-binary A/B), e.g. GVRT_OPTS=compact_nodes=1
+        r.set_option(name, int(val))
     # the bench's default quality build (GVRT_BUILD=fast: device LBVH)
     r.prepare(s, **({} if os.environ.get("GVRT_BUILD") == "fast" else dict(builder=2, collapse=1)))
     for _ in range(n):
