@@ -438,14 +438,16 @@ __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlan
                         const float al = acc ? galpha : -1.0f;                                                     \
                         /* (an inclusive tmin exists only in LITERAL mode: the API refuses it otherwise) */        \
                         const bool incl = LITERAL && a.tmin_inclusive;                                             \
-                        bool in0 = (incl ? tn >= tlo : tn > tlo) && tn <= thi;                                     \
-                        bool in1 = (incl ? tf >= tlo : tf > tlo) && tf <= thi;                                     \
+                        bool in0 = (incl ? tn >= tlo : tn > tlo) & (tn <= thi);                                    \
+                        bool in1 = (incl ? tf >= tlo : tf > tlo) & (tf <= thi);                                    \
                         if (uni(pa.y) != 0xFFFFFFFFu) {                                                            \
                             in0 = in0 && crossing_cell(o, d, tn, a, pa.z, pa.w) == pa.y;                           \
                             in1 = in1 && crossing_cell(o, d, tf, a, pa.z, pa.w) == pa.y;                           \
                         }                                                                                          \
-                        const float ta = in0 && tn < tcut ? tn : (in1 && tf < tcut ? tf : INF_DIST);               \
-                        const float tb = (in0 && in1 && tf < tcut) ? tf : INF_DIST;                                \
+                        /* (bitwise &: short-circuit && became exec-mask branches around these selects) */         \
+                        const bool c0 = in0 & (tn < tcut), c1 = in1 & (tf < tcut);                                 \
+                        const float ta = c0 ? tn : (c1 ? tf : INF_DIST);                                           \
+                        const float tb = (c0 & c1) ? tf : INF_DIST;  /* tn <= tf: in0 & in1 & tf < tcut */         \
                         if (ta < kt[KB - 1]) {                                                                     \
                           if constexpr (PACK) {                                                                    \
                             const uint32_t q = alpha_code(galpha);                                                 \
@@ -454,15 +456,9 @@ __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlan
                             /* whose running sum reaches qneed is the last one composited; no */                   \
                             /* slot can reach it while the inserted total is still below */                        \
                             qtot += tb < INF_DIST ? 2 * q : q;                                                     \
-                            if (__builtin_amdgcn_ballot_w64(qtot >= qneed)) {                                      \
-                            uint32_t qs = 0;                                                                       \
-                            float tt = INF_DIST;                                                                   \
-_Pragma("unroll")                                                                                                  \
-                            for (int i = 0; i < KB; ++i) {                                                         \
-                                qs += kid[i] & 0xFFu;                                                              \
-                                tt = fminf(tt, qs >= qneed ? kt[i] : INF_DIST);                                    \
-                            }                                                                                      \
-                            tcut = fminf(tcut, tt);                                                                \
+                            if (GVRT_WALK_PER_NODE) walk_due = true;                                               \
+                            else if (__builtin_amdgcn_ballot_w64(qtot >= qneed)) {                                 \
+                                TERM_WALK                                                                          \
                             }                                                                                      \
                           } else {                                                                                 \
                             kb_insert2<KB>(ta, tb, gi, al, kt, kid, ka);                                           \
@@ -487,6 +483,43 @@ _Pragma("unroll")                                                               
             }                                                                                                      \
         }                                                                                                          \
     }
+
+// termination walk (kb_insert2p's cull): the first slot whose running q sum reaches qneed bounds what can still be
+// composited.  GVRT_WALK_PER_NODE (A/B builds): walk once after a node's leaves instead of after every insertion (a
+// staler cull is still conservative: it only admits crossings past the termination point, which are never composited)
+#ifndef GVRT_WALK_PER_NODE
+#define GVRT_WALK_PER_NODE 0
+#endif
+#ifndef GVRT_WALK3
+#define GVRT_WALK3 0
+#endif
+#if GVRT_WALK3
+// 3 VALU per slot: g = (qneed - running q sum) x 2^100 as a float (exact: integers below 2^24 times a power of two),
+// one v_cvt_f32_ubyte0 + one FMA per slot; med3(kt, g, tt) keeps tt while g > 0 (g >= 2^100 > any t) and takes
+// min(kt, tt) once g <= 0, so with kt ascending tt ends at the first slot whose sum reaches qneed, as the compare /
+// select / min form (qneed above 24 x 255 can never be reached and is clamped to 8191, which keeps that)
+#define TERM_WALK                                                                           \
+    {                                                                                       \
+        float g = (float)(qneed < 8191u ? qneed : 8191u) * 0x1p100f;                         \
+        float tt = INF_DIST;                                                                \
+        _Pragma("unroll") for (int i = 0; i < KB; ++i) {                                    \
+            g = fmaf((float)(kid[i] & 0xFFu), -0x1p100f, g);                                \
+            tt = __builtin_amdgcn_fmed3f(kt[i], g, tt);                                     \
+        }                                                                                   \
+        tcut = fminf(tcut, tt);                                                             \
+    }
+#else
+#define TERM_WALK                                                  \
+    {                                                              \
+        uint32_t qs = 0;                                           \
+        float tt = INF_DIST;                                       \
+        _Pragma("unroll") for (int i = 0; i < KB; ++i) {           \
+            qs += kid[i] & 0xFFu;                                  \
+            tt = fminf(tt, qs >= qneed ? kt[i] : INF_DIST);        \
+        }                                                          \
+        tcut = fminf(tcut, tt);                                    \
+    }
+#endif
 
 constexpr uint32_t ST_W = 8, ST_H = 4;
 constexpr int RENDER_MIN_WAVES = 4;
@@ -772,11 +805,15 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                 s_tph[1] = t;
             }
             // ---- leaves of this node (the k-buffer orders them); one rolled loop = one insertion site
+            [[maybe_unused]] bool walk_due = false;
 #pragma unroll 1
             while (leafmask) {
                 const int k = __builtin_ctz(leafmask);
                 leafmask &= leafmask - 1;
                 GVRT_LEAF(~GVRT_PICK(ch, k), GVRT_PICK(bal, k))  // leaf slot, lanes whose ray hits its box
+            }
+            if constexpr (PACK && GVRT_WALK_PER_NODE) {
+                if (__builtin_amdgcn_ballot_w64(walk_due && qtot >= qneed)) TERM_WALK
             }
             if constexpr (STATS) wadd(C_LEAF, __builtin_amdgcn_s_memtime() - s_tph[1]);
             if (next < 0) break;
