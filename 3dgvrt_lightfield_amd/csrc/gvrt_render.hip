@@ -456,10 +456,7 @@ __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlan
                             /* whose running sum reaches qneed is the last one composited; no */                   \
                             /* slot can reach it while the inserted total is still below */                        \
                             qtot += tb < INF_DIST ? 2 * q : q;                                                     \
-                            if (GVRT_WALK_PER_NODE) walk_due = true;                                               \
-                            else if (__builtin_amdgcn_ballot_w64(qtot >= qneed)) {                                 \
-                                TERM_WALK                                                                          \
-                            }                                                                                      \
+                            if (__builtin_amdgcn_ballot_w64(qtot >= qneed)) TERM_WALK                             \
                           } else {                                                                                 \
                             kb_insert2<KB>(ta, tb, gi, al, kt, kid, ka);                                           \
                             /* Termination-aware cull distance: walking the sorted slots with the */               \
@@ -484,20 +481,12 @@ __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlan
         }                                                                                                          \
     }
 
-// termination walk (kb_insert2p's cull): the first slot whose running q sum reaches qneed bounds what can still be
-// composited.  GVRT_WALK_PER_NODE (A/B builds): walk once after a node's leaves instead of after every insertion (a
-// staler cull is still conservative: it only admits crossings past the termination point, which are never composited)
-#ifndef GVRT_WALK_PER_NODE
-#define GVRT_WALK_PER_NODE 0
-#endif
-#ifndef GVRT_WALK3
-#define GVRT_WALK3 0
-#endif
-#if GVRT_WALK3
-// 3 VALU per slot: g = (qneed - running q sum) x 2^100 as a float (exact: integers below 2^24 times a power of two),
-// one v_cvt_f32_ubyte0 + one FMA per slot; med3(kt, g, tt) keeps tt while g > 0 (g >= 2^100 > any t) and takes
-// min(kt, tt) once g <= 0, so with kt ascending tt ends at the first slot whose sum reaches qneed, as the compare /
-// select / min form (qneed above 24 x 255 can never be reached and is clamped to 8191, which keeps that)
+// Termination walk (kb_insert2p's cull): the first slot whose running q sum reaches qneed bounds what can still be
+// composited.  3 VALU per slot: g = (qneed - running sum) x 2^100 as a float (exact: integers below 2^24 times a power of
+// two), one v_cvt_f32_ubyte0 + one FMA per slot; med3(kt, g, tt) keeps tt while g > 0 (g >= 2^100 > any t) and takes
+// min(kt, tt) once g <= 0, so with kt ascending tt ends at the first slot whose sum reaches qneed -- the compare /
+// select / min form's result with a quarter fewer instructions (qneed above 24 x 255 can never be reached and is
+// clamped to 8191, which keeps that).  Same-box: dense -1.2 %, bicycle -0.3 % (profiles/r05/ab/ab_walk_branchfree.log)
 #define TERM_WALK                                                                           \
     {                                                                                       \
         float g = (float)(qneed < 8191u ? qneed : 8191u) * 0x1p100f;                         \
@@ -508,18 +497,6 @@ __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlan
         }                                                                                   \
         tcut = fminf(tcut, tt);                                                             \
     }
-#else
-#define TERM_WALK                                                  \
-    {                                                              \
-        uint32_t qs = 0;                                           \
-        float tt = INF_DIST;                                       \
-        _Pragma("unroll") for (int i = 0; i < KB; ++i) {           \
-            qs += kid[i] & 0xFFu;                                  \
-            tt = fminf(tt, qs >= qneed ? kt[i] : INF_DIST);        \
-        }                                                          \
-        tcut = fminf(tcut, tt);                                    \
-    }
-#endif
 
 constexpr uint32_t ST_W = 8, ST_H = 4;
 constexpr int RENDER_MIN_WAVES = 4;
@@ -805,15 +782,11 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                 s_tph[1] = t;
             }
             // ---- leaves of this node (the k-buffer orders them); one rolled loop = one insertion site
-            [[maybe_unused]] bool walk_due = false;
 #pragma unroll 1
             while (leafmask) {
                 const int k = __builtin_ctz(leafmask);
                 leafmask &= leafmask - 1;
                 GVRT_LEAF(~GVRT_PICK(ch, k), GVRT_PICK(bal, k))  // leaf slot, lanes whose ray hits its box
-            }
-            if constexpr (PACK && GVRT_WALK_PER_NODE) {
-                if (__builtin_amdgcn_ballot_w64(walk_due && qtot >= qneed)) TERM_WALK
             }
             if constexpr (STATS) wadd(C_LEAF, __builtin_amdgcn_s_memtime() - s_tph[1]);
             if (next < 0) break;

@@ -42,7 +42,8 @@ with gv.Renderer(0) as r:
                      "accepted/ray": round(st["accepted"] / rays, 3), "rounds/ray": round(st["rounds"] / rays, 3),
                      "node_visits/wave": round(st["wave_node_visits"] / waves, 1),
                      "leaf_visits/wave": round(st["wave_leaf_visits"] / waves, 1),
-                     "dead_visits/wave": round(st["wave_dead_visits"] / waves, 1),
+                     "dead_visits/wave": round((st["wave_dead_visits"] & 0xFFFFFFFF) / waves, 1),
+                     "pruned_pops/wave": round((st["wave_dead_visits"] >> 32) / waves, 1),
                      "rounds/wave": round(st["wave_rounds"] / waves, 3),
                      "late_node_visits/wave": round(st["wave_late_node_visits"] / waves, 1),
                      "lane_leaf_tests/ray": round(st["lane_leaf_tests"] / rays, 2), "bvh_depth": st["bvh_depth"], "bvh_nodes": st["bvh_nodes"], "bvh_leaves": st["bvh_leaves"], "accel_ms": round(st["accel_ms"], 2)}
