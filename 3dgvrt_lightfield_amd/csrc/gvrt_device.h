@@ -15,7 +15,7 @@ namespace gvrt {
 
 constexpr float EPS_T = 1e-9f;                        // 3dgs.glsl:13
 constexpr int K_HITS = 16;                            // MAX_HIT_PER_TRACE, 3dgs.glsl:15
-constexpr int K_FAST_DEFAULT = 24;                    // FAST k-buffer depth (fewer rounds; same image)
+constexpr int K_FAST_DEFAULT = 32;                    // FAST k-buffer depth (fewer rounds; same image)
 constexpr uint32_t INVALID_ID = 0xFFFFFFFFu;          // 3dgs.glsl:26
 constexpr float INF_DIST = 1e20f;                     // 3dgs.glsl:27
 constexpr float KERNEL_S = -0.0555555555556f;         // degree-4 response, gaussianfunctions.glsl:31-35

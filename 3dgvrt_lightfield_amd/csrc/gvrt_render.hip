@@ -18,7 +18,7 @@
 // on a 128-entry per-wave LDS stack.  Leaves are tested response first (an accepted crossing passes inside
 // the proxy's inscribed sphere), then clipped against the analytic icosahedron (10 antipodal slab pairs in
 // the kernel frame), which yields the same two crossings (entry and exit face, Q1) as the reference's
-// 20-triangle proxy.  Each lane keeps a register k-buffer (FAST: 24 slots of {t, record id << 8 | q},
+// 20-triangle proxy.  Each lane keeps a register k-buffer (FAST: 32 slots of {t, record id << 8 | q},
 // q a conservative optical-depth code that drives the termination cull; LITERAL: the reference's 16 slots
 // of every crossing, anyhit.rahit:29-71).  After each traversal round every lane composites its slots front
 // to back (processHit, gaussianfunctions.glsl:153-229) with the SH basis of its ray direction precomputed
@@ -49,7 +49,7 @@ static_assert(BVH_W == 4, "the render kernel traverses 4-wide nodes");
 
 // Composite tuning (same-box A/B): the first SH_EARLY of a hit's 12 SH float4 loads are summed
 // before the accept branch (round 2: issued with the record's, -1.5 %; the ROCm 7.2 compiler sinks them into the
-// branch again, and forcing 3 or 6 of them out with an asm anchor measured +0.5-1 % in round 4); the FAST K = 24
+// branch again, and forcing 3 or 6 of them out with an asm anchor measured +0.5-1 % in round 4); a FAST K = 24
 // buffer is composited in groups of COMP_GROUP slots (static register indices, one buffer shift per group).
 constexpr int SH_EARLY = 6;
 constexpr int COMP_GROUP = 6;
@@ -811,7 +811,7 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                 // the buffer shifts down by CUN between groups.  Per lane: stop at the first empty slot
                 // or once T <= minTransmittance (slots are sorted with the empty ones last, T only falls).
                 bool go = true;
-                // groups of 6 for the default FAST depth (fewer shifts; spill-free there), else 4
+                // groups of 6 at K = 24 (fewer shifts), else 4 (K = 32: 8 spills, 6 measured even)
                 constexpr int CUN = (PACK && KB == 24) ? COMP_GROUP : 4;
 #pragma unroll 1
                 for (int base = 0; base < KB; base += CUN) {
@@ -825,13 +825,14 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                         bool hacc;
                         hid = PACK ? (kid[j] >> 8) : kid[j];
                         // the SH address needs only the id: all 12 loads in one batch, one memory round trip
-                        // instead of one per dependent chunk (see SH_EARLY for where the compiler issues them)
+                        // instead of one per dependent chunk (see SH_EARLY for where the compiler issues them);
+                        // K = 32 loads the second half after the first (48 VGPRs of SH spilled the buffer)
+                        constexpr int SH_FIRST = (PACK && KB > 24) ? 6 : 12;
+                        static_assert(SH_FIRST >= SH_EARLY && SH_FIRST % 3 == 0, "the early chunks are loaded first");
                         float4 shv[12];
-                        {
-                            const float4* s4 = reinterpret_cast<const float4*>(sh_ + 48ull * hid);
+                        const float4* s4 = reinterpret_cast<const float4*>(sh_ + 48ull * hid);
 #pragma unroll
-                            for (int q = 0; q < 12; ++q) shv[q] = s4[q];
-                        }
+                        for (int q = 0; q < SH_FIRST; ++q) shv[q] = s4[q];
                         if constexpr (PACK) {
                             // processHit re-evaluates the response of the hit particle (per-lane record load)
                             const RenderRec rec = crecw[hid];
@@ -856,6 +857,11 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
                             }
                         }
                         if (hacc) {
+                            if constexpr (SH_FIRST < 12) {
+                                asm volatile("" ::: "memory");
+#pragma unroll
+                                for (int q = SH_FIRST; q < 12; ++q) shv[q] = s4[q];
+                            }
                             const float weight = halpha * T;
                             float rr = er, rg = eg, rb = eb;
 #pragma unroll
@@ -1028,7 +1034,7 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
         if (adaptive) GVRT_LAUNCH(false, true, K_HITS, false);
         else GVRT_LAUNCH(false, false, K_HITS, false);
     } else if (adaptive) {
-        GVRT_LAUNCH(false, true, K_FAST_DEFAULT, true);
+        GVRT_LAUNCH(false, true, 24, true);  // adaptive leaves at K = 32 spilled 8 B/lane
     } else {
         // FAST: the k-buffer depth only sets the number of traversal rounds, not the image
         switch (a.kfast) {
@@ -1036,7 +1042,7 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
             case 12: GVRT_LAUNCH_F(12); break;
             case 16: GVRT_LAUNCH_F(16); break;
             case 20: GVRT_LAUNCH_F(20); break;
-            case 32: GVRT_LAUNCH_F(32); break;
+            case 24: GVRT_LAUNCH_F(24); break;
             default:
                 // the default depth also reads kernel-frame origins from the records when render_impl
                 // prepared them for a single-origin launch (RenderArgs::okrec)

@@ -865,7 +865,7 @@ def main():
         if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
             # FETCH_SIZE in KiB, half-counted on gfx950 (x2); WRITE_SIZE in KiB (MI355X_MICROARCH.md, HBM)
             traffic = pmc["FETCH_SIZE"] * 1024 * 2 + pmc["WRITE_SIZE"] * 1024
-        kern = "k_render<FAST,K=24,packed>" if args.mode == "fast" else "k_render<LITERAL,K=16>"
+        kern = "k_render<FAST,K=32,packed>" if args.mode == "fast" else "k_render<LITERAL,K=16>"
         if pmc and "SQ_INSTS_VALU" in pmc and pmc.get("GRBM_GUI_ACTIVE"):
             cyc = pmc["GRBM_GUI_ACTIVE"] / N_XCD  # shader cycles of the dispatch
             clock = cyc / (kern_avg * 1e-3)

@@ -71,7 +71,7 @@ typedef struct {
     uint32_t mode;                   /* GVRT_MODE_FAST (default) or GVRT_MODE_LITERAL */
     uint32_t max_rounds;             /* 0 = unlimited */
     uint32_t ray_dirs_layout;        /* 0: [cam][y][x]; 1: light-field [cam][x][y] (raygenGaussianLightField.rgen:129) */
-    uint32_t kbuffer_depth;          /* FAST only: 0 = default (24); 8, 12, 16, 20, 24 or 32 slots per ray (sets
+    uint32_t kbuffer_depth;          /* FAST only: 0 = default (32); 8, 12, 16, 20, 24 or 32 slots per ray (sets
                                         the number of traversal rounds, not the image) */
     uint32_t reserved[4];
 } gvrt_render_params;
