@@ -263,6 +263,7 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
     if (p->collapse > 1) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "collapse must be 0 (greedy) or 1 (SAH-optimal DP)");
     GVRT_HIP(c, hipSetDevice(c->device));
     c->okrecs_valid[0] = c->okrecs_valid[1] = false;
+    c->okrecs_full[0] = c->okrecs_full[1] = false;
     c->recs_cams_ok = false;
     c->okrecs_nomem = c->recs_cams_nomem = false;
     c->leaf_hk_ok = false;
@@ -633,6 +634,14 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
     // every queued launch that read it), so a static camera records none; a slot's event is waited for only when
     // the ring comes round to it with its readers still queued (CAM_RING camera changes deep)
     if ((s = ensure_cameras(c, ncams))) return s;
+    float* cam_pending = nullptr;  // one camera's ring slot still to be written
+    struct CamGuard {  // a return before the slot is written: the next launch uploads the camera again
+        gvrt_context* c;
+        float* const* p;
+        ~CamGuard() {
+            if (*p) c->cam_valid = false;
+        }
+    } cam_guard{c, &cam_pending};
     if (!c->cam_valid || c->h_viewinv.size() != 16ull * ncams ||
         std::memcmp(c->h_viewinv.data(), view_inverse, 64ull * ncams) != 0) {
         if (c->cam_valid) {
@@ -641,10 +650,15 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         }
         const uint32_t slot = (c->cam_slot + 1) % gvrt_context::CAM_RING;
         if (c->cam_ev_live[slot]) GVRT_HIP(c, hipEventSynchronize(c->cam_ev[slot]));
-        float* src = c->h_viewinv_pin + slot * c->cam_stride;
-        std::memcpy(src, view_inverse, 64ull * ncams);
-        GVRT_HIP(c, hipMemcpyAsync(c->d_viewinv + slot * c->cam_stride, src, 64ull * ncams, hipMemcpyHostToDevice,
-                                   c->stream));
+        if (ncams == 1) {
+            // written by this launch's k_rec_origin pass when it has one (a moving camera), else copied below
+            cam_pending = c->d_viewinv + slot * c->cam_stride;
+        } else {
+            float* src = c->h_viewinv_pin + slot * c->cam_stride;
+            std::memcpy(src, view_inverse, 64ull * ncams);
+            GVRT_HIP(c, hipMemcpyAsync(c->d_viewinv + slot * c->cam_stride, src, 64ull * ncams,
+                                       hipMemcpyHostToDevice, c->stream));
+        }
         c->h_viewinv.assign(view_inverse, view_inverse + 16ull * ncams);
         c->cam_slot = slot;
         c->cam_valid = true;
@@ -750,6 +764,7 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
             for (int j = 0; j < 2; ++j) {
                 gvrt_dfree(c, (void**)&c->d_okrecs[j]);
                 c->okrecs_valid[j] = false;
+                c->okrecs_full[j] = false;
             }
             c->okrecs_n = 0;
             bool ok = true;
@@ -780,7 +795,11 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
                 // the copy not used by the latest launch, rewritten in stream order (after its queued readers);
                 // a side stream overlapping the pass with the previous frame measured slower
                 k = c->okrecs_valid[c->okrecs_cur] ? 1 - c->okrecs_cur : c->okrecs_cur;
-                if ((s = gvrt_launch_rec_origin(c, view_inverse + 12, c->d_okrecs[k], c->stream))) return s;
+                if ((s = gvrt_launch_rec_origin(c, view_inverse + 12, c->d_okrecs[k], c->stream, cam_pending,
+                                                view_inverse, c->okrecs_full[k])))
+                    return s;
+                cam_pending = nullptr;
+                c->okrecs_full[k] = true;
                 std::memcpy(c->okrecs_origin[k], view_inverse + 12, 12);
                 c->okrecs_valid[k] = true;
             }
@@ -788,6 +807,12 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
             a.recs = c->d_okrecs[k];
             a.crecs = c->d_okrecs[k];
         }
+    }
+    if (cam_pending) {
+        float* src = c->h_viewinv_pin + (uint64_t)(cam_pending - c->d_viewinv);
+        std::memcpy(src, view_inverse, 64);
+        GVRT_HIP(c, hipMemcpyAsync(cam_pending, src, 64, hipMemcpyHostToDevice, c->stream));
+        cam_pending = nullptr;
     }
     if (a.kfast != 8 && a.kfast != 12 && a.kfast != 16 && a.kfast != 20 && a.kfast != 24 && a.kfast != 32)
         return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "kbuffer_depth must be 0, 8, 12, 16, 20, 24 or 32");

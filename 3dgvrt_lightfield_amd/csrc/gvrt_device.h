@@ -73,6 +73,10 @@ __host__ __device__ inline f3 cross3(f3 a, f3 b) {
 }
 
 // Render-kernel launch arguments (one struct, passed by value).
+struct CamArg {  // one camera matrix as a by-value kernel argument
+    float v[16];
+};
+
 struct RenderArgs {
     const RenderRec* __restrict__ recs;  // leaf order (one per BVH leaf)
     const RenderRec* __restrict__ crecs; // by k-buffer id: = recs, or the compaction order when split

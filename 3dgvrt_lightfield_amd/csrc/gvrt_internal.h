@@ -68,6 +68,7 @@ struct gvrt_context {
     uint64_t okrecs_n = 0;
     float okrecs_origin[2][3] = {{0, 0, 0}, {0, 0, 0}};
     bool okrecs_valid[2] = {false, false};
+    bool okrecs_full[2] = {false, false};  // every field but the origin equals d_recs (a pass may write 12 B)
     int okrecs_cur = 0;
     bool okrecs_nomem = false;  // the copies did not fit (until the next build): launches read d_recs
     // multi-origin launches (light-field rigs): one record copy per camera with that camera's kernel-frame origins,
@@ -178,8 +179,11 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const gvrt::RenderArgs& a, 
 // codes: the tile list the order is over (cam << 24 | ty << 12 | tx); radius > 0: classes spread by a max filter
 gvrt_status gvrt_launch_tile_order(gvrt_context* c, const uint32_t* codes, int radius);
 // record preparation: op 0 save leaf positions, 1 write kernel-frame origins for o, 2 restore positions
-// k_rec_origin: dst = d_recs with each position replaced by the kernel-frame origin of o, on `stream`
-gvrt_status gvrt_launch_rec_origin(gvrt_context* c, const float* o, gvrt::RenderRec* dst, hipStream_t stream);
+// k_rec_origin: dst = d_recs with each position replaced by the kernel-frame origin of o, on `stream`; with cam_dst
+// it also writes the 16 floats at cam into cam_dst (the launch's camera slot); pos_only: dst already holds the
+// other fields of every record (only the three origin floats are written)
+gvrt_status gvrt_launch_rec_origin(gvrt_context* c, const float* o, gvrt::RenderRec* dst, hipStream_t stream,
+                                   float* cam_dst = nullptr, const float* cam = nullptr, bool pos_only = false);
 // multi-origin launches: per-camera record copies (dst = ncams x n_leaves records) for the cameras at d_view_inv
 gvrt_status gvrt_launch_rec_cams(gvrt_context* c, uint32_t ncams, const float* d_view_inv, gvrt::RenderRec* dst);
 // adaptive enclosing: d_leaf_hk from the leaf records (k_leaf_hk)

@@ -1137,8 +1137,11 @@ __global__ __launch_bounds__(256) void k_tile_order(uint32_t n, const uint8_t* _
 // position the largest class within R tiles, with the class counts for k_tile_order.
 __global__ __launch_bounds__(256) void k_tile_scatter(uint32_t n, const uint32_t* __restrict__ codes,
                                                       const uint8_t* __restrict__ bucket, uint32_t tiles_x,
-                                                      uint32_t tiles_y, uint8_t* __restrict__ grid) {
+                                                      uint32_t tiles_y, uint8_t* __restrict__ grid,
+                                                      uint32_t* __restrict__ hist_dilated) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    // the dilated class counts k_tile_dilate adds into (the previous launch's k_tile_order has read them)
+    if (i < TILE_BUCKETS) hist_dilated[i] = 0u;
     if (i >= n) return;
     const uint32_t t = codes[i];
     grid[((uint64_t)(t >> 24) * tiles_y + ((t >> 12) & 0xFFFu)) * tiles_x + (t & 0xFFFu)] = bucket[i];
@@ -1179,10 +1182,10 @@ gvrt_status gvrt_launch_tile_order(gvrt_context* c, const uint32_t* codes, int r
     uint32_t* hist = h + TILE_BUCKETS * p;
     if (radius > 0 && codes) {
         const uint64_t cells = (uint64_t)c->ord_tx * c->ord_ty * c->ord_nc;
-        GVRT_HIP(c, hipMemsetAsync(c->d_tgrid, 0, cells, c->stream));
-        GVRT_HIP(c, hipMemsetAsync(h + 4 * TILE_BUCKETS, 0, 4 * TILE_BUCKETS, c->stream));
+        // a list covering every tile writes every grid cell; a partial one leaves the others at class 0
+        if (n < cells) GVRT_HIP(c, hipMemsetAsync(c->d_tgrid, 0, cells, c->stream));
         hipLaunchKernelGGL(k_tile_scatter, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, codes, c->d_tbucket,
-                           c->ord_tx, c->ord_ty, c->d_tgrid);
+                           c->ord_tx, c->ord_ty, c->d_tgrid, h + 4 * TILE_BUCKETS);
         hipLaunchKernelGGL(k_tile_dilate, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, codes, c->d_tgrid,
                            c->ord_tx, c->ord_ty, radius, c->d_tbucket2, h + 4 * TILE_BUCKETS);
         bucket = c->d_tbucket2;
@@ -1200,12 +1203,22 @@ gvrt_status gvrt_launch_tile_order(gvrt_context* c, const uint32_t* codes, int r
 // Record copies for FAST launches: each leaf record with its position replaced by its kernel-frame origin
 // ok = S^-1 R^T (o - p) of the launch camera (kernel_org, the arithmetic the render kernel would otherwise do per
 // leaf visit and per composited hit).  d_recs keeps the positions.
+// (cam_dst: the camera ring slot this launch's render reads, written from the kernel argument: a moving camera then
+// needs no separate host-to-device copy in the stream)
 __global__ __launch_bounds__(256) void k_rec_origin(uint64_t m, const RenderRec* __restrict__ src, RenderRec* dst,
-                                                    float ox, float oy, float oz) {
+                                                    float ox, float oy, float oz, float* __restrict__ cam_dst,
+                                                    const CamArg cam, uint32_t pos_only) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cam_dst && i < 16) cam_dst[i] = cam.v[i];
     if (i >= m) return;
     RenderRec r = src[i];
     const f3 ok = kernel_org(r, mk3(ox, oy, oz));
+    if (pos_only) {  // the copy's other fields already equal src's: 12 of the 64 bytes written
+        dst[i].px = ok.x;
+        dst[i].py = ok.y;
+        dst[i].pz = ok.z;
+        return;
+    }
     r.px = ok.x;
     r.py = ok.y;
     r.pz = ok.z;
@@ -1256,11 +1269,17 @@ gvrt_status gvrt_launch_rec_cams(gvrt_context* c, uint32_t ncams, const float* d
     return GVRT_OK;
 }
 
-gvrt_status gvrt_launch_rec_origin(gvrt_context* c, const float* o, RenderRec* dst, hipStream_t stream) {
+gvrt_status gvrt_launch_rec_origin(gvrt_context* c, const float* o, RenderRec* dst, hipStream_t stream,
+                                   float* cam_dst, const float* cam, bool pos_only) {
     const uint64_t m = c->n_leaves;
     if (!m) return GVRT_OK;
+    CamArg ca;
+    CamArg ca0 = {};
+    ca = ca0;
+    if (cam_dst)
+        for (int k = 0; k < 16; ++k) ca.v[k] = cam[k];
     hipLaunchKernelGGL(k_rec_origin, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, m, c->d_recs, dst,
-                       o[0], o[1], o[2]);
+                       o[0], o[1], o[2], cam_dst, ca, pos_only ? 1u : 0u);
     GVRT_HIP(c, hipGetLastError());
     return GVRT_OK;
 }
