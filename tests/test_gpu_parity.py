@@ -734,6 +734,29 @@ def test_multi_origin_record_copies_change_no_pixel(gv, config1):
     assert np.abs(outs[1][0] - outs[1][3]).max() > 0  # the moved rig sees something else
 
 
+def test_origin_record_copies_across_a_rebuild(gv, config1):
+    """A record copy that already holds every field writes only the new origin's three floats (k_rec_origin
+    pos_only), and the moving camera's slot is written by that same pass.  A rebuild on another scene of the same
+    size must make the next pass write whole records again: frames before and after the rebuild, for new and returning
+    origins, equal the record_origins = 0 path bit for bit."""
+    W, H = 96, 64
+    other = gv.scene.make(kind="config1", n=10_000, seed=7)
+    eyes = [(0.0, 0.3, 3.2), (0.5, 0.2, 3.0), (-0.4, 0.5, 3.3), (0.0, 0.3, 3.2)]
+    cams = [gv.camera.pinhole(e, (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 40.0, W / H) for e in eyes]
+    outs = {}
+    for ro in (1, 0):
+        with gv.Renderer(0) as r:
+            r.set_option("record_origins", ro)
+            got = []
+            for scene in (config1, other, config1):
+                r.prepare(scene)
+                got += [r.render(vi, pi, W, H, rgba8=False)["rgba32f"] for vi, pi in cams]
+        outs[ro] = got
+    for a, b in zip(outs[1], outs[0]):
+        np.testing.assert_array_equal(a, b)
+    assert np.abs(outs[1][0] - outs[1][4]).max() > 0  # the other scene renders something else
+
+
 def test_origin_record_copies_queued_moving_camera(gv, config1):
     """Single-origin FAST launches read one of two origin record copies; a new camera origin is written, in
     stream order, into the copy the latest launch did not use.  Eight frames queued back to back
