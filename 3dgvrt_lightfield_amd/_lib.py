@@ -80,18 +80,19 @@ class Image(C.Structure):
 
 class AccelParams(C.Structure):
     _fields_ = [("split_cells", C.c_uint32), ("builder", C.c_uint32), ("collapse", C.c_uint32),
-                ("reserved", C.c_uint32 * 5)]
+                ("depth_budget", C.c_uint32), ("reserved", C.c_uint32 * 4)]
 
 
 class Stats(C.Structure):
     _fields_ = [("n_input", C.c_uint64), ("n_survivors", C.c_uint64), ("bvh_nodes", C.c_uint64),
-                ("bvh_depth", C.c_uint32), ("pad0", C.c_uint32), ("rays", C.c_uint64),
+                ("bvh_depth", C.c_uint32), ("bvh_depth4", C.c_uint32), ("rays", C.c_uint64),
                 ("crossings", C.c_uint64), ("accepted", C.c_uint64), ("rounds", C.c_uint64),
                 ("enclose_ms", C.c_float), ("accel_ms", C.c_float), ("render_ms", C.c_float),
                 ("pad1", C.c_float), ("device_bytes", C.c_uint64), ("wave_node_visits", C.c_uint64),
                 ("wave_leaf_visits", C.c_uint64), ("lane_leaf_tests", C.c_uint64),
                 ("phase_cycles", C.c_uint64 * 4), ("wave_dead_visits", C.c_uint64),
-                ("bvh_leaves", C.c_uint64), ("wave_rounds", C.c_uint64), ("wave_late_node_visits", C.c_uint64)]
+                ("bvh_leaves", C.c_uint64), ("wave_rounds", C.c_uint64), ("wave_late_node_visits", C.c_uint64),
+                ("bvh_builder", C.c_uint32), ("bvh_depth4_rebuilt", C.c_uint32)]
 
 
 class DeviceProperties(C.Structure):

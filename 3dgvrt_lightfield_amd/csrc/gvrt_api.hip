@@ -261,6 +261,8 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
         return gvrt_fail(c, GVRT_ERR_INVALID_ARG,
                          "builder must be 0 (LBVH), 1 (PLOC), 2 (binned SAH, device) or 3 (binned SAH, host)");
     if (p->collapse > 1) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "collapse must be 0 (greedy) or 1 (SAH-optimal DP)");
+    if (p->depth_budget > gvrt::SAH_DEPTH_MAX)
+        return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "depth_budget must be 0 (default) or at most 43");
     GVRT_HIP(c, hipSetDevice(c->device));
     c->okrecs_valid[0] = c->okrecs_valid[1] = false;
     c->okrecs_full[0] = c->okrecs_full[1] = false;

@@ -24,6 +24,19 @@ constexpr float IPHI = 0.618033988749895f;
 constexpr float ICOSA_VRT_SCALE = 0.5f * 1.323169076499215f;  // particlePrimitives.comp:78-79
 constexpr float SQRT3 = 1.7320508075688772f;
 constexpr int STACK_DEPTH = 128;                      // per-wave LDS traversal stack
+// Depth budget of the SAH builds (device gvrt_sah.hip and its host checker): max binary leaf depth, root at depth 1.
+// A range of n proxies at depth d keeps d + ceil(log2 n) <= SAH_DEPTH_MAX: a SAH split whose larger side would break
+// it halves the (Morton-ordered) range instead, which keeps it.  So the binary tree, and with it the 4-wide tree
+// (every 4-wide level descends at least one binary level), stays within the traversal stack at any M and any
+// geometry.  Trees of the stand-in scenes are 30-33 deep: the budget never fires there, their builds are unchanged.
+constexpr uint32_t SAH_DEPTH_MAX = 43;
+static_assert((4 - 1) * (SAH_DEPTH_MAX - 1) + 2 <= (uint32_t)STACK_DEPTH, "the 4-wide depth bound fits the stack");
+__host__ __device__ inline uint32_t ceil_log2(uint32_t n) { return n <= 1 ? 0u : 32u - (uint32_t)__builtin_clz(n - 1u); }
+// a split of a range at depth d into sides of nl and nr proxies keeps the budget dmax (<= SAH_DEPTH_MAX;
+// gvrt_accel_params.depth_budget tightens it for tests)
+__host__ __device__ inline bool sah_split_in_budget(uint32_t d, uint32_t nl, uint32_t nr, uint32_t dmax) {
+    return d + 1u + ceil_log2(nl > nr ? nl : nr) <= dmax;
+}
 constexpr int TILE_CPO = 4;                           // cost classes per octave of the cost-ordered dispatch
 constexpr int TILE_BUCKETS = 16 * TILE_CPO;           // classes: 1 k .. 64 M cycles
 

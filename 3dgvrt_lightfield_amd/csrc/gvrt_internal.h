@@ -171,7 +171,8 @@ gvrt_status gvrt_ploc_build(gvrt_context* c, uint32_t m, const float* leaf_boxes
                             int32_t* leaf_parent, int32_t* node_parent, int32_t* root, uint32_t* iterations);
 // gvrt_sah.hip (the quality build on the device: binned SAH + SAH-optimal collapse)
 gvrt_status gvrt_sah_build_device(gvrt_context* c, uint64_t m, const float* lboxes, gvrt::BvhNode* nodes,
-                                  gvrt::Bvh4Node* out4, uint32_t* depth_out, uint64_t* n4_out, uint32_t* depth4_out);
+                                  gvrt::Bvh4Node* out4, uint32_t* depth_out, uint64_t* n4_out, uint32_t* depth4_out,
+                                  uint32_t dmax);
 // gvrt_render.hip
 // the render launch; ev_start / ev_stop are recorded at the kernel's start and end (its kernel time)
 gvrt_status gvrt_launch_render_mode(gvrt_context* c, const gvrt::RenderArgs& a, uint64_t nwaves, bool literal,

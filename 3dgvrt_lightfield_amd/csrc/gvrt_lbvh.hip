@@ -477,7 +477,7 @@ static float host_area(const float* b) {
 // the lower side of the recorded split axis, leaves as ~(leaf index).
 // keep != null: the tree stays on the host for the host-side collapse (no upload / download round trip)
 static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lboxes, int32_t* root,
-                                  std::vector<BvhNode>* keep) {
+                                  std::vector<BvhNode>* keep, uint32_t dmax) {
     std::vector<float> bx(6 * m);
     GVRT_HIP(c, hipMemcpyAsync(bx.data(), d_lboxes, 24 * m, hipMemcpyDeviceToHost, c->stream));
     GVRT_HIP(c, hipStreamSynchronize(c->stream));
@@ -511,7 +511,7 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
     // and the right child is id + L — independent of the order ranges are processed in, so subtrees
     // build on several threads with the same result
     std::vector<BvhNode> nodes(m - 1);
-    struct Task { uint32_t b, e, node; };
+    struct Task { uint32_t b, e, node, d; };  // d: binary depth of the range's node (root 1)
     auto split = [&](const Task& t, Task* kids, int& nk) {
         uint32_t mid = t.b + (t.e - t.b) / 2;
         int axis = 0;
@@ -522,6 +522,7 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
                 ch[a] = std::max(ch[a], cen[3 * idx[i] + a]);
             }
         int best_axis = -1, best_split = 0;
+        uint32_t best_nl = 0;
         float best_cost = INFINITY;
         for (int a = 0; a < 3; ++a) {
             const float ext = ch[a] - cl[a];
@@ -558,9 +559,13 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
                     best_cost = cost;
                     best_axis = a;
                     best_split = k;
+                    best_nl = n;
                 }
             }
         }
+        // depth budget (SAH_DEPTH_MAX, as the device build): halve instead of a split whose larger side could not
+        // finish in budget
+        if (best_axis >= 0 && !sah_split_in_budget(t.d, best_nl, (t.e - t.b) - best_nl, dmax)) best_axis = -1;
         if (best_axis >= 0) {
             axis = best_axis;
             const float sc = NB / (ch[axis] - cl[axis]);
@@ -569,7 +574,7 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
                 return std::min(NB - 1, (int)((cen[3 * p + axis] - cl[axis]) * sc)) <= best_split;
             });
             mid = (uint32_t)(it - idx.begin());
-        }  // else every centroid equal: halve the range
+        }  // else every centroid equal, or the depth budget: halve the range
         Box lb, rb;
         lb.reset();
         rb.reset();
@@ -586,9 +591,9 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
         const uint32_t L = mid - t.b;
         nk = 0;
         if (L == 1) nd.c0 = ~(int32_t)idx[t.b];
-        else { nd.c0 = (int32_t)(t.node + 1); kids[nk++] = {t.b, mid, t.node + 1}; }
+        else { nd.c0 = (int32_t)(t.node + 1); kids[nk++] = {t.b, mid, t.node + 1, t.d + 1}; }
         if (t.e - mid == 1) nd.c1 = ~(int32_t)idx[mid];
-        else { nd.c1 = (int32_t)(t.node + L); kids[nk++] = {mid, t.e, t.node + L}; }
+        else { nd.c1 = (int32_t)(t.node + L); kids[nk++] = {mid, t.e, t.node + L, t.d + 1}; }
         nd.pad0 = (uint32_t)axis;
         nd.pad1 = 0;
     };
@@ -606,7 +611,7 @@ static gvrt_status host_sah_build(gvrt_context* c, uint64_t m, const float* d_lb
     // the top of the tree breadth-first on this thread until there is work for every thread, then the
     // subtrees on a small pool
     const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::vector<Task> front{{0u, (uint32_t)m, 0u}}, next;
+    std::vector<Task> front{{0u, (uint32_t)m, 0u, 1u}}, next;
     while (!front.empty() && front.size() < 4 * nth) {
         next.clear();
         for (const Task& t : front) {
@@ -779,6 +784,9 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
         c->stats.bvh_nodes = 0;
         c->stats.bvh_leaves = 0;
         c->stats.bvh_depth = 0;
+        c->stats.bvh_depth4 = 0;
+        c->stats.bvh_builder = ap.builder;
+        c->stats.bvh_depth4_rebuilt = 0;
         return GVRT_OK;
     }
     if (mp > 0x7FFFFFFFll) return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "more than 2^31-1 survivors");
@@ -968,6 +976,11 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
         const bool sah_dev = !ploc && !sah_host && ap.builder == 2;
         const bool dp = ap.collapse == 1;
         std::vector<BvhNode> htree;  // SAH tree kept on the host for the DP collapse
+        // the SAH builds' depth budget (gvrt_accel_params.depth_budget: 0 = SAH_DEPTH_MAX); one the leaves cannot
+        // meet (1 + ceil(log2 m) levels are needed) is refused
+        const uint32_t dmax = ap.depth_budget ? ap.depth_budget : SAH_DEPTH_MAX;
+        if ((sah_host || sah_dev) && 1u + ceil_log2((uint32_t)m) > dmax)
+            TRY(gvrt_fail(c, GVRT_ERR_INVALID_ARG, "depth_budget below 1 + ceil(log2(leaves))"));
         int32_t root = 0;
         uint32_t sah_depth = 0, sah_d4 = 0;
         uint64_t sah_n4 = 0;
@@ -975,10 +988,10 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
             uint32_t iters = 0;
             TRY(gvrt_ploc_build(c, (uint32_t)m, lboxes, c->d_nodes, lpar, npar, &root, &iters));
         } else if (sah_host) {
-            TRY(host_sah_build(c, (uint64_t)m, lboxes, &root, dp ? &htree : nullptr));
+            TRY(host_sah_build(c, (uint64_t)m, lboxes, &root, dp ? &htree : nullptr, dmax));
         } else if (sah_dev) {
             TRY(gvrt_sah_build_device(c, (uint64_t)m, lboxes, c->d_nodes, dp ? c->d_nodes4 : nullptr, &sah_depth,
-                                      &sah_n4, &sah_d4));
+                                      &sah_n4, &sah_d4, dmax));
         } else {
             // leaf-range union table, then the hierarchy with its child boxes in one pass (no refit)
             hlv[0] = lboxes;
@@ -1058,12 +1071,26 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
     cleanup();
 #undef TRY
 #undef TRYH
-    // the traversal pushes at most BVH_W - 1 entries per level
-    if ((BVH_W - 1) * c->depth4 + 2 > (uint32_t)STACK_DEPTH)
-        return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "LBVH deeper than the render kernel's traversal stack");
+    // the traversal pushes at most BVH_W - 1 entries per level.  The SAH builds (2, 3) keep the depth budget by
+    // construction (SAH_DEPTH_MAX); an LBVH or PLOC tree too deep for the stack (clustered, multi-scale geometry) is
+    // rebuilt by the device SAH build with the same collapse and split options instead of refusing the scene
+    if ((BVH_W - 1) * c->depth4 + 2 > (uint32_t)STACK_DEPTH) {
+        if (ap.builder == 0 || ap.builder == 1) {
+            gvrt_accel_params q = ap;
+            q.builder = 2;
+            const uint32_t d4 = c->depth4;
+            const gvrt_status s2 = gvrt_launch_build_accel(c, q);
+            c->stats.bvh_depth4_rebuilt = d4;
+            return s2;
+        }
+        return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "BVH deeper than the render kernel's traversal stack");
+    }
     c->stats.bvh_nodes = c->n_nodes4;
     c->stats.bvh_leaves = c->n_leaves;
     c->stats.bvh_depth = c->depth;
+    c->stats.bvh_depth4 = c->depth4;
+    c->stats.bvh_builder = ap.builder;
+    c->stats.bvh_depth4_rebuilt = 0;
     c->accel = true;
     return GVRT_OK;
 }

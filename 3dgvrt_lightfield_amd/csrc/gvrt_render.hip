@@ -485,10 +485,12 @@ __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlan
 // composited.  3 VALU per slot: g = (qneed - running sum) x 2^100 as a float (exact: integers below 2^24 times a power of
 // two), one v_cvt_f32_ubyte0 + one FMA per slot; med3(kt, g, tt) keeps tt while g > 0 (g >= 2^100 > any t) and takes
 // min(kt, tt) once g <= 0, so with kt ascending tt ends at the first slot whose sum reaches qneed -- the compare /
-// select / min form's result with a quarter fewer instructions (qneed above 24 x 255 can never be reached and is
-// clamped to 8191, which keeps that).  Same-box: dense -1.2 %, bicycle -0.3 % (profiles/r05/ab/ab_walk_branchfree.log)
+// select / min form's result with a quarter fewer instructions (qneed above KB x 255 can never be reached and is
+// clamped to 8191, which keeps that while KB x 255 < 8191: K <= 32, asserted).  Same-box: dense -1.2 %, bicycle -0.3 %
+// (profiles/r05/ab/ab_walk_branchfree.log)
 #define TERM_WALK                                                                           \
     {                                                                                       \
+        static_assert(KB * 255 < 8191, "the qneed clamp must stay above any reachable q sum"); \
         float g = (float)(qneed < 8191u ? qneed : 8191u) * 0x1p100f;                         \
         float tt = INF_DIST;                                                                \
         _Pragma("unroll") for (int i = 0; i < KB; ++i) {                                    \
@@ -1036,7 +1038,9 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
     } else if (adaptive) {
         GVRT_LAUNCH(false, true, 24, true);  // adaptive leaves at K = 32 spilled 8 B/lane
     } else {
-        // FAST: the k-buffer depth only sets the number of traversal rounds, not the image
+        // FAST: the k-buffer depth sets the number of traversal rounds; it can also move rays whose tie or threshold
+        // decisions the oracle flags (a round boundary falls elsewhere), so the 24 -> 32 default change altered
+        // a few flagged garden and dense rgba8 pixels (tests/test_gpu_frame_digest.py)
         switch (a.kfast) {
             case 8: GVRT_LAUNCH_F(8); break;
             case 12: GVRT_LAUNCH_F(12); break;
@@ -1165,6 +1169,7 @@ __global__ __launch_bounds__(256) void k_tile_dilate(uint32_t n, const uint32_t*
     uint32_t m = 0;
     for (int y = y0; y <= y1; ++y)
         for (int x = x0; x <= x1; ++x) m = max(m, (uint32_t)g[(uint64_t)y * tiles_x + x]);
+    m = min(m, (uint32_t)(TILE_BUCKETS - 1));  // cnt[] / k_tile_order's classes are TILE_BUCKETS wide
     out[i] = (uint8_t)m;
     atomicAdd(&cnt[m], 1u);
     }
@@ -1182,8 +1187,9 @@ gvrt_status gvrt_launch_tile_order(gvrt_context* c, const uint32_t* codes, int r
     uint32_t* hist = h + TILE_BUCKETS * p;
     if (radius > 0 && codes) {
         const uint64_t cells = (uint64_t)c->ord_tx * c->ord_ty * c->ord_nc;
-        // a list covering every tile writes every grid cell; a partial one leaves the others at class 0
-        if (n < cells) GVRT_HIP(c, hipMemsetAsync(c->d_tgrid, 0, cells, c->stream));
+        // the handle's own full-frame list (d_tcode: every tile exactly once) writes every grid cell; a caller's
+        // list may be partial or repeat tiles, so the cells it does not write are cleared to class 0 first
+        if (codes != c->d_tcode || n < cells) GVRT_HIP(c, hipMemsetAsync(c->d_tgrid, 0, cells, c->stream));
         hipLaunchKernelGGL(k_tile_scatter, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, codes, c->d_tbucket,
                            c->ord_tx, c->ord_ty, c->d_tgrid, h + 4 * TILE_BUCKETS);
         hipLaunchKernelGGL(k_tile_dilate, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, codes, c->d_tgrid,

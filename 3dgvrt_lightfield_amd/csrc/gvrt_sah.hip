@@ -209,6 +209,7 @@ struct BuildOut {
     uint32_t* tiny_n;
     Task* large_q;    // ranges above LARGE (next level of the chunked path)
     uint32_t* large_n;
+    uint32_t dmax;    // depth budget (SAH_DEPTH_MAX or gvrt_accel_params.depth_budget)
 };
 
 // Write node t.node with split s (mid = left end) and queue its children; lane 0 writes.  first_l /
@@ -304,6 +305,8 @@ __global__ __launch_bounds__(64 * SMALL_WAVES) void k_sah_mid(const Task* __rest
                 }
             }
             s = sah_eval(B, sc);
+            // depth budget (SAH_DEPTH_MAX): a split whose larger side could not finish in budget halves instead
+            if (s.k >= 0 && !sah_split_in_budget(t.db >> 1, s.nl, n - s.nl, o.dmax)) s.axis = -1, s.k = -1;
         }
         uint32_t mid, first_l = 0xFFFFFFFFu, first_r = 0xFFFFFFFFu;
         if (s.k >= 0) {
@@ -325,7 +328,7 @@ __global__ __launch_bounds__(64 * SMALL_WAVES) void k_sah_mid(const Task* __rest
                 rb += __popcll(br);
             }
         } else {
-            // every centroid equal: halve the range, boxes of the halves
+            // every centroid equal, or the depth budget: halve the range, boxes of the halves
             mid = t.b + n / 2;
             for (uint32_t i = t.b + lane; i < t.e; i += 64) dst[i] = src[i];
             wave_box_union(boxes, src, t.b, mid, s.lb);
@@ -366,7 +369,8 @@ __device__ inline float union_area(const float* lb, const float* rb) {
 __global__ __launch_bounds__(64 * SMALL_WAVES) void k_sah_tiny(const Task* __restrict__ q, const uint32_t* __restrict__ qn,
                                                               const uint32_t* __restrict__ idx0, const uint32_t* __restrict__ idx1,
                                                               const float* __restrict__ boxes, BvhNode* __restrict__ nodes,
-                                                              float4* __restrict__ F, uint32_t* __restrict__ maxd) {
+                                                              float4* __restrict__ F, uint32_t* __restrict__ maxd,
+                                                              uint32_t dmax) {
     __shared__ Bins sb[SMALL_WAVES];
     __shared__ uint32_t s_rng[SMALL_WAVES][TINY];  // stack: lb | le << 8 | local node id << 16
     __shared__ uint32_t s_dep[SMALL_WAVES][TINY];
@@ -453,6 +457,7 @@ __global__ __launch_bounds__(64 * SMALL_WAVES) void k_sah_tiny(const Task* __res
                     }
                 }
                 s = sah_eval(B, sc);
+                if (s.k >= 0 && !sah_split_in_budget(dep, s.nl, nn - s.nl, dmax)) s.axis = -1, s.k = -1;  // depth budget
                 if (s.k >= 0) left = act && sah_bin(cen[s.axis], cl[s.axis], sc[s.axis]) <= s.k;
             }
             uint32_t mid;
@@ -646,7 +651,7 @@ struct Decision {
     uint32_t mid;
 };
 __global__ __launch_bounds__(64) void k_lg_eval(const Task* __restrict__ tasks, const LgRange* __restrict__ r,
-                                                Decision* __restrict__ dec) {
+                                                Decision* __restrict__ dec, uint32_t dmax) {
     const uint32_t t = blockIdx.x;
     float cl[3], sc[3];
     range_scales(r[t], cl, sc);
@@ -656,6 +661,8 @@ __global__ __launch_bounds__(64) void k_lg_eval(const Task* __restrict__ tasks, 
     s.nl = 0;
     if (sc[0] > 0.0f || sc[1] > 0.0f || sc[2] > 0.0f) s = sah_eval(r[t].bins, sc);
     const Task tk = tasks[t];
+    // depth budget (SAH_DEPTH_MAX): halve the range instead of a split whose larger side could not finish in budget
+    if (s.k >= 0 && !sah_split_in_budget(tk.db >> 1, s.nl, (tk.e - tk.b) - s.nl, dmax)) s.axis = -1, s.k = -1;
     if ((threadIdx.x & 63) == 0) {
         Decision d;
         d.s = s;
@@ -892,7 +899,7 @@ struct DevBuf {
 // max binary leaf depth; with out4 != null also the surface-area-optimal 4-wide collapse into out4
 // (*n4 nodes, *depth4 levels).
 gvrt_status gvrt_sah_build_device(gvrt_context* c, uint64_t m, const float* lboxes, BvhNode* nodes, Bvh4Node* out4,
-                                  uint32_t* depth_out, uint64_t* n4_out, uint32_t* depth4_out) {
+                                  uint32_t* depth_out, uint64_t* n4_out, uint32_t* depth4_out, uint32_t dmax) {
     if (m < 2) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "device SAH build needs two or more leaves");
     if (m > 0x7FFFFFFFull) return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "device SAH build: too many leaves");
     const bool dp = out4 != nullptr;
@@ -935,7 +942,7 @@ gvrt_status gvrt_sah_build_device(gvrt_context* c, uint64_t m, const float* lbox
         }
         GVRT_HIP(c, hipStreamSynchronize(st));
     }
-    BuildOut o{nodes, ctl.p + 3, midq.p, ends.p + 1, tinyq.p, ctl.p + 0, nullptr, ctl.p + 2};
+    BuildOut o{nodes, ctl.p + 3, midq.p, ends.p + 1, tinyq.p, ctl.p + 0, nullptr, ctl.p + 2, dmax};
     // ---- chunked levels: host-side list of the level's large ranges (a handful per level), logged for the DP
     std::vector<Task> lt = m > LARGE ? std::vector<Task>{Task{0u, (uint32_t)m, 0u, 1u << 1}} : std::vector<Task>{};
     std::vector<Task> hlog;
@@ -959,7 +966,7 @@ gvrt_status gvrt_sah_build_device(gvrt_context* c, uint64_t m, const float* lbox
         hipLaunchKernelGGL(k_lg_init, dim3(nr), dim3(256), 0, st, lr.p, nr);
         hipLaunchKernelGGL(k_lg_cbounds, dim3(nc), dim3(256), 0, st, chunks.p, lcur, idx0.p, idx1.p, lboxes, lr.p);
         hipLaunchKernelGGL(k_lg_bin, dim3(nc), dim3(256), 0, st, chunks.p, lcur, idx0.p, idx1.p, lboxes, lr.p);
-        hipLaunchKernelGGL(k_lg_eval, dim3(nr), dim3(64), 0, st, lcur, lr.p, dec.p);
+        hipLaunchKernelGGL(k_lg_eval, dim3(nr), dim3(64), 0, st, lcur, lr.p, dec.p, dmax);
         hipLaunchKernelGGL(k_lg_count, dim3(nc), dim3(256), 0, st, chunks.p, lcur, idx0.p, idx1.p, lboxes, lr.p, dec.p,
                            nleft.p);
         hipLaunchKernelGGL(k_lg_scatter, dim3(nc), dim3(256), 0, st, chunks.p, lcur, idx0.p, idx1.p, lboxes, lr.p, dec.p,
@@ -996,7 +1003,7 @@ gvrt_status gvrt_sah_build_device(gvrt_context* c, uint64_t m, const float* lbox
     if (!done) return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "device SAH build did not finish");
     // ---- tiny subtrees (with their DP rows)
     hipLaunchKernelGGL(k_sah_tiny, dim3(grid), dim3(64 * SMALL_WAVES), 0, st, tinyq.p, ctl.p + 0, idx0.p, idx1.p,
-                       lboxes, nodes, dp ? F.p : nullptr, ctl.p + 3);
+                       lboxes, nodes, dp ? F.p : nullptr, ctl.p + 3, dmax);
     GVRT_HIP(c, hipGetLastError());
     GVRT_HIP(c, hipMemcpyAsync(depth_out, ctl.p + 3, 4, hipMemcpyDeviceToHost, st));
     if (!dp) {

@@ -22,8 +22,9 @@
 // exchange (sending what its part buffer holds), drains it, and then aborts its communicator.  ncclCommAbort does not
 // notify peers over P2P / SHM links, so every wait on the exchange is bounded instead of trusting that: wait() polls
 // the stream and ncclCommGetAsyncError against a deadline (set_timeout, default 120 s) and aborts the communicator
-// when it passes, so a peer that is gone costs its partners at most the timeout, never a hang.  The multi-rank
-// failure paths are exercised on one rank only (two ranks cannot share one GPU under RCCL).
+// when it passes.  The bound covers the waits SplitFrame itself makes; draw() calls wait() for the previous frame
+// before it queues the next render, so the render call's own host waits (camera-ring events, tile-list uploads)
+// never sit behind an exchange whose peer is gone.
 #pragma once
 #include <rccl/rccl.h>
 

@@ -123,10 +123,11 @@ class Renderer:
             out["verts"], out["tris"] = verts, tris
         return out
 
-    def build_accel(self, split_cells=0, builder=0, collapse=0):
+    def build_accel(self, split_cells=0, builder=0, collapse=0, depth_budget=0):
         p = _lib.AccelParams()
         lib().gvrt_default_accel_params(C.byref(p))
         p.split_cells, p.builder, p.collapse = int(split_cells), int(builder), int(collapse)
+        p.depth_budget = int(depth_budget)
         check(lib().gvrt_build_accel_ex(self.h, C.byref(p)), self.h)
 
     def prepare(self, splats, split_cells=0, builder=0, collapse=0, **enclosing):

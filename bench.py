@@ -42,6 +42,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table
+L2_PEAK_GBS = 34500.0  # aggregate L2 of the 8 XCDs (MI355X_MICROARCH.md, L2 per XCD: ~34.5 TB/s)
+L2_LAT_CYC = 200.0     # global_load L2-hit latency, ~180-225 cycles (MI355X_MICROARCH.md, per-instruction constants)
 # VALU issue: 256 CUs x 4 SIMD-32s, a wave64 VALU instruction occupies its SIMD for 2 cycles (MI355X_MICROARCH.md);
 # the clock is the one measured over the dispatch (GRBM_GUI_ACTIVE counts cycles on each of the 8 XCDs)
 N_SIMD = 256 * 4
@@ -88,7 +90,8 @@ def parse():
                          "ranks in cost bands and exchanged to rank 0; 'none' to skip")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the `configs` sub-record of the default one-GPU line (garden, truck 4K, light field, dense, "
-                         "orbit 0.5 deg: kernel ms, Mrays/s, VALU issue, logical fraction, first frame)")
+                         "trained stand-in, orbit 0.5 and 2 deg: kernel ms, Mrays/s, VALU issue, visits per wave, "
+                         "first frame)")
     ap.add_argument("--configs-child", action="store_true", help=argparse.SUPPRESS)  # PMC child of the configs record
     ap.add_argument("--pmc-keep", default=None, metavar="DIR",
                     help="keep the per-dispatch PMC rows of the line's own passes as DIR/bench_pmc.json (profiles/)")
@@ -157,7 +160,11 @@ def pmc_passes(args):
     # (8 SQ counters and 1 GRBM counter fit one pass; FETCH_SIZE / WRITE_SIZE need TCC passes of their own)
     passes = [["FETCH_SIZE"], ["WRITE_SIZE"],
               ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY",
-               "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "GRBM_GUI_ACTIVE"]]
+               "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "GRBM_GUI_ACTIVE"],
+              # what the kernel asks of the cache hierarchy: L2 requests and hits, the scalar cache,
+              # the vector L1 (3 TCC, 2 TCP, 2 SQ, 1 GRBM counters: within one pass's limits)
+              ["TCC_REQ_sum", "TCC_HIT_sum", "TCC_MISS_sum", "TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum",
+               "SQC_DCACHE_REQ", "SQC_DCACHE_MISSES", "GRBM_GUI_ACTIVE"]]
     tmp = tempfile.mkdtemp(prefix="gvrt_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
         for i, counters in enumerate(passes):
@@ -205,8 +212,9 @@ def pmc_passes(args):
 # the headline's protocol (first frame alone, then W warm-up and K timed frames queued back to back, barrier-free one
 # GPU).  (label, scene config, camera path)
 CONFIG_SET = (("garden", "garden", "static"), ("truck_4k", "truck", "static"), ("lightfield_16", "lightfield", "static"),
-              ("dense", "dense", "static"), ("orbit_0.5deg", "bicycle", "orbit"))
-ORBIT_STEP = 0.5
+              ("dense", "dense", "static"), ("trained", "trained", "static"), ("orbit_0.5deg", "bicycle", "orbit"),
+              ("orbit_2deg", "bicycle", "orbit"))
+ORBIT_STEPS = {"orbit_0.5deg": 0.5, "orbit_2deg": 2.0}  # degrees of azimuth per frame of the orbit entries
 
 
 def scene_cached(gv, gen):
@@ -226,14 +234,14 @@ def scene_cached(gv, gen):
     return sp
 
 
-def config_frames(gv, name, path, nframes):
+def config_frames(gv, name, path, nframes, step=0.5):
     """Per-frame cameras of one configs-record entry: the config camera (config 5: the centred 16-view rig, as
-    `--config lightfield`), or for the orbit path azimuth 30 + k * ORBIT_STEP in frame k."""
+    `--config lightfield`), or for the orbit path azimuth 30 + k * step in frame k."""
     _, W, H, ncams = gv.scene.CONFIGS[name]
     views = ncams if name == "lightfield" else 1
 
     def rig(k):
-        az = 30.0 + (k * ORBIT_STEP if path == "orbit" else 0.0)
+        az = 30.0 + (k * step if path == "orbit" else 0.0)
         v, p = gv.camera.lightfield_grid_rig(gv.camera.orbit_eye(4.0, 20.0, az), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0),
                                              nx=views, ny=1, spacing=0.1, fovy_deg=50.0,
                                              aspect=gv.camera.aspect_ratio(W, H), centred=name == "lightfield")
@@ -263,7 +271,8 @@ def run_config_set(gv, torch, steps, warmup, bicycle_r=None, literal=True, bkw=N
             r, own = gv.Renderer(dev.index), True
             m = r.prepare(scenes[key], **(bkw or {}))
         nframes = 1 + warmup + steps
-        frames, W, H, views = config_frames(gv, name, path, nframes)
+        step = ORBIT_STEPS.get(label, 0.5)
+        frames, W, H, views = config_frames(gv, name, path, nframes, step)
         params = r.render_params(mode=gv.MODE_FAST)
         buf = torch.zeros((views * H * W * 4,), dtype=torch.uint8, device=dev)
         torch.cuda.synchronize()
@@ -287,7 +296,7 @@ def run_config_set(gv, torch, steps, warmup, bicycle_r=None, literal=True, bkw=N
         kms = float(r.render_ms())
         rays = W * H * views
         rec = {"config": f"{name}: {gen['n']} Gaussians ({m} survivors), {W}x{H}" + (f" x {views} views" if views > 1 else "")
-                         + (f", camera orbiting {ORBIT_STEP} deg per frame" if path == "orbit" else ""),
+                         + (f", camera orbiting {step} deg per frame" if path == "orbit" else ""),
                "rays_per_step": rays, "kernel_ms": round(kms, 4), "ms_per_step": round(el / steps * 1e3, 4),
                "mrays": round(rays * steps / el / 1e6, 1), "kernel_mrays": round(rays / (kms * 1e-3) / 1e6, 1),
                "first_frame_kernel_ms": round(first_ms, 4), "first_frame_wall_ms": round(first_wall, 4)}
@@ -301,8 +310,19 @@ def run_config_set(gv, torch, steps, warmup, bicycle_r=None, literal=True, bkw=N
             st = r.stats()
             r.set_stats(False)
             b = 48.0 * st["crossings"] + 192.0 * st["accepted"] + 4.0 * rays
-            rec["logical_frac"] = round(b / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-            rec["algorithmic_bytes_per_launch"] = b
+            # the reference algorithm's gather bytes (no fraction: packet traversal shares them, see the roofline)
+            rec["reference_gather_bytes"] = b
+            rec["reference_gather_equiv_gbs"] = round(b / (kms * 1e-3) / 1e9, 1)
+            # traversal diagnostics of the product traversal (the FAST counter kernel): visits per wave
+            r.set_stats(True)
+            r.render(frames[0][0], frames[0][1], W, H, views, params=r.render_params(mode=gv.MODE_FAST),
+                     rgba8=False, rgba32f=False)
+            sf = r.stats()
+            r.set_stats(False)
+            waves = views * ((W + 7) // 8) * ((H + 7) // 8)
+            rec["node_visits_per_wave"] = round(sf["wave_node_visits"] / waves, 2)
+            rec["leaf_visits_per_wave"] = round(sf["wave_leaf_visits"] / waves, 2)
+            rec["rounds_per_wave"] = round(sf["wave_rounds"] / waves, 3)
         manifest.append([label, nframes])
         recs[label] = rec
         del buf
@@ -841,11 +861,15 @@ def main():
         # moves ~0.2 GB per launch through HBM (2-3 % of 8 TB/s) and its waves spend their lifetime issuing (~42 %),
         # waiting on dependent scalar loads (~38 %) or ready behind other waves' issue (~20 %); the busiest unit is
         # the SIMDs' VALU pipe: frac = 2 x VALU wave-instructions / (1024 SIMDs x the dispatch's cycles), <= 1 by
-        # construction.  roofline.logical keeps SURVEY §8d's algorithmic-bytes figure of round 1-3 (the reference
-        # algorithm's gather bytes, from the LITERAL counters: above 1 on scenes where packet traversal shares most
-        # gathers across a wave's 64 rays, so it is no bound).
+        # construction.  Beside it what the kernel asks of the cache hierarchy (L2 requests against
+        # the L2 peak, the scalar cache, the vector L1) and a latency account (dependent scalar loads per wave x the
+        # L2 hit latency / the wave lifetime); `binding` names the largest of the three fractions.
+        # roofline.reference_gather keeps SURVEY §8d's algorithmic bytes (the reference algorithm's one-ray-at-a-time
+        # gathers, from the LITERAL counters) as a plain figure: packet traversal shares those gathers across a wave's
+        # 64 rays, so it is neither a bound nor a physical rate.
         roof = None
         lit_stats = None
+        fast_stats = None
         logical = None
         vi = frame_vi[0]  # the frame-0 camera (the static headline's) for the counters and the CPU baseline
         if not args.no_stats:
@@ -857,10 +881,15 @@ def main():
             bytes_per_launch = (48.0 * lit_stats["crossings"] + 192.0 * lit_stats["accepted"] + 4.0 * rays1) * (
                 rays_per_rank / rays1)
             achieved = bytes_per_launch / (kern_avg * 1e-3) / 1e9
-            logical = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                       "frac": round(achieved / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_launch": bytes_per_launch,
-                       "note": "SURVEY §8d: sum over rays of 48 B per crossing + 192 B per accepted crossing + 4 B, the "
-                               "reference algorithm's counters; not a bound (packet traversal shares the gathers)"}
+            logical = {"bytes_per_launch": bytes_per_launch, "equivalent_gbs": round(achieved, 1),
+                       "note": "SURVEY §8d: sum over rays of 48 B per crossing + 192 B per accepted crossing + 4 B (the "
+                               "reference algorithm's LITERAL counters) / kernel time.  Not a bound and not a physical "
+                               "rate: the packet traversal issues one scalar gather per wave where this counts 64"}
+            # the product traversal's visits (FAST counter kernel, same traversal as the timed kernel)
+            r.set_stats(True)
+            r.render(vi[:16], pi, W, H, 1, params=r.render_params(mode=gv.MODE_FAST), rgba8=False, rgba32f=False)
+            fast_stats = r.stats()
+            r.set_stats(False)
         traffic = None
         if pmc and "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
             # FETCH_SIZE in KiB, half-counted on gfx950 (x2); WRITE_SIZE in KiB (MI355X_MICROARCH.md, HBM)
@@ -885,8 +914,9 @@ def main():
                 roof["wave_cycles"] = {"issuing": round(pmc.get("SQ_ACTIVE_INST_ANY", 0) / wc, 4),
                                        "waiting_on_memory": round(pmc.get("SQ_WAIT_ANY", 0) / wc, 4),
                                        "ready_not_issued": round(pmc.get("SQ_WAIT_INST_ANY", 0) / wc, 4)}
-        elif logical:  # no PMC passes (--no-pmc or rocprofv3 missing): the logical figure stands in
-            roof = {**logical, "traffic": traffic, "note": "no PMC passes: " + str((pmc or {}).get("error", "--no-pmc"))}
+        else:  # no PMC passes (--no-pmc or rocprofv3 missing): nothing measured binds
+            roof = {"bound": "unmeasured", "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": traffic,
+                    "note": "no PMC passes: " + str((pmc or {}).get("error", "--no-pmc"))}
         if roof is not None and traffic is not None and "wave_cycles" in roof:
             # the binding unit is the busier of the two measured resources: VALU issue or HBM bytes
             hbm_frac = traffic / (kern_avg * 1e-3) / 1e9 / HBM_PEAK_GBS
@@ -897,7 +927,48 @@ def main():
             roof["kernel_ms_avg"] = round(kern_avg, 4)
             roof["kernel"] = kern
             if logical:
-                roof["logical"] = logical
+                roof["reference_gather"] = logical
+            if pmc and pmc.get("TCC_REQ_sum") is not None and pmc.get("SQ_WAVES"):
+                # L2 (TCC) requests: each moves at most one 128-B line, so req x 128 B bounds the bytes L2 served
+                l2_bytes = pmc["TCC_REQ_sum"] * 128.0
+                l2_gbs = l2_bytes / (kern_avg * 1e-3) / 1e9
+                hits = pmc.get("TCC_HIT_sum", 0.0)
+                miss = pmc.get("TCC_MISS_sum", 0.0)
+                sq_req = pmc.get("SQC_DCACHE_REQ", 0.0)
+                roof["cache"] = {
+                    "l2_requests": pmc["TCC_REQ_sum"], "l2_hit_rate": round(hits / max(hits + miss, 1.0), 4),
+                    "l2_request_bytes_max": l2_bytes, "l2_gbs_max": round(l2_gbs, 1), "l2_peak_gbs": L2_PEAK_GBS,
+                    "l2_frac": round(l2_gbs / L2_PEAK_GBS, 4),
+                    "scalar_loads": pmc.get("SQ_INSTS_SMEM"),
+                    "scalar_request_bytes": pmc.get("SQ_INSTS_SMEM", 0.0) * 64.0,
+                    "scalar_cache_requests": sq_req,
+                    "scalar_cache_hit_rate": round(1.0 - pmc.get("SQC_DCACHE_MISSES", 0.0) / max(sq_req, 1.0), 4),
+                    "vector_l1_accesses": pmc.get("TCP_TOTAL_CACHE_ACCESSES_sum"),
+                    "vector_l1_to_l2_reads": pmc.get("TCP_TCC_READ_REQ_sum"),
+                    "note": "per launch.  Scalar loads are the wave-uniform node (2 x 64 B) and leaf-record (64 B) "
+                            "fetches; vector L1 accesses are the per-lane record and SH loads of the composite; L2 "
+                            "serves both.  l2_frac = TCC_REQ_sum x 128 B / kernel time / the guide's 34.5 TB/s L2 peak "
+                            "(an upper bound on the bytes: a request moves at most one line)"}
+            if fast_stats and pmc and pmc.get("SQ_WAVE_CYCLES") and pmc.get("SQ_WAVES"):
+                waves = pmc["SQ_WAVES"]
+                life = 4.0 * pmc["SQ_WAVE_CYCLES"] / waves  # SQ_WAVE_CYCLES counts quad-cycles
+                nv = fast_stats["wave_node_visits"] / waves
+                lv = fast_stats["wave_leaf_visits"] / waves
+                roof["latency"] = {
+                    "node_visits_per_wave": round(nv, 2), "leaf_visits_per_wave": round(lv, 2),
+                    "rounds_per_wave": round(fast_stats["wave_rounds"] / waves, 3),
+                    "wave_lifetime_cycles": round(life, 1), "l2_hit_latency_cycles": L2_LAT_CYC,
+                    "frac": round((nv + lv) * L2_LAT_CYC / life, 4),
+                    "note": "each node and leaf visit waits for one dependent scalar load (a node's two loads issue "
+                            "together); frac = (node + leaf visits per wave) x the guide's L2-hit latency / the wave's "
+                            "lifetime (4 x SQ_WAVE_CYCLES / SQ_WAVES): the share of a wave's life spent waiting on the "
+                            "chain if every load hit L2 (Infinity Cache hits take ~545 cycles)"}
+            fr = {"valu_issue": roof.get("valu_issue_frac", roof["frac"]) if roof["bound"] == "hbm" else roof["frac"],
+                  "l2_bandwidth": roof.get("cache", {}).get("l2_frac"),
+                  "dependent_load_latency": roof.get("latency", {}).get("frac")}
+            fr = {k: v for k, v in fr.items() if v is not None}
+            if fr:
+                roof["binding"] = {"fractions": fr, "largest": max(fr, key=fr.get)}
             if traffic is not None:
                 hb = traffic / (kern_avg * 1e-3) / 1e9
                 roof["hbm"] = {"achieved": round(hb, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -1003,8 +1074,10 @@ def main():
                     rec["valu_issue_frac"] = None
             configs["_note"] = (f"each config timed as the headline ({args.warmup} warm-up + {args.steps} timed frames "
                                 "queued back to back after an unordered first frame); valu_issue_frac from one rocprofv3 SQ "
-                                "pass of a child rendering the same set (5 timed frames each); logical_frac = SURVEY §8d "
-                                f"bytes / kernel time / 8 TB/s; whole record {time.perf_counter() - t_cfg:.1f} s")
+                                "pass of a child rendering the same set (5 timed frames each); reference_gather_* = SURVEY "
+                                "§8d bytes of the reference's one-ray-at-a-time gathers (LITERAL counters), not a physical "
+                                "rate; node / leaf visits and rounds per wave from the FAST counter kernel; whole record "
+                                f"{time.perf_counter() - t_cfg:.1f} s")
             if cfg_pmc and "error" in cfg_pmc:
                 configs["_pmc_error"] = cfg_pmc["error"]
         if cache_dir:

@@ -71,8 +71,10 @@ typedef struct {
     uint32_t mode;                   /* GVRT_MODE_FAST (default) or GVRT_MODE_LITERAL */
     uint32_t max_rounds;             /* 0 = unlimited */
     uint32_t ray_dirs_layout;        /* 0: [cam][y][x]; 1: light-field [cam][x][y] (raygenGaussianLightField.rgen:129) */
-    uint32_t kbuffer_depth;          /* FAST only: 0 = default (32); 8, 12, 16, 20, 24 or 32 slots per ray (sets
-                                        the number of traversal rounds, not the image) */
+    uint32_t kbuffer_depth;          /* FAST only: 0 = default (32); 8, 12, 16, 20, 24 or 32 slots per ray.  Sets
+                                        the number of traversal rounds; rays whose tie or threshold decisions the
+                                        oracle flags can move with it (the 24 -> 32 default change altered a few
+                                        such garden and dense rgba8 pixels) */
     uint32_t reserved[4];
 } gvrt_render_params;
 
@@ -100,8 +102,8 @@ typedef struct {
     uint64_t n_input;      /* N */
     uint64_t n_survivors;  /* M (ParticleCounts) */
     uint64_t bvh_nodes;    /* internal nodes */
-    uint32_t bvh_depth;    /* max leaf depth */
-    uint32_t pad0;
+    uint32_t bvh_depth;    /* max leaf depth of the binary tree (root 1) */
+    uint32_t bvh_depth4;   /* levels of the 4-wide tree the render kernel traverses */
     uint64_t rays;         /* last render */
     uint64_t crossings;    /* processed crossings (X), last render; only with stats enabled */
     uint64_t accepted;     /* accepted crossings (A) */
@@ -120,6 +122,9 @@ typedef struct {
     uint64_t bvh_leaves;        /* BVH leaves: the survivors, or their grid-cell pieces when split */
     uint64_t wave_rounds;       /* traversal rounds summed over waves (stats enabled) */
     uint64_t wave_late_node_visits; /* node visits in the second and later rounds of a wave */
+    uint32_t bvh_builder;       /* the builder that made the tree: the requested one, or 2 (device SAH) when an
+                                   LBVH / PLOC tree was too deep for the traversal stack */
+    uint32_t bvh_depth4_rebuilt; /* 4-wide levels of that too-deep tree (0: the requested builder's tree was kept) */
 } gvrt_stats;
 
 /* --------------------------------------------------------------------------------------- */
@@ -160,12 +165,18 @@ gvrt_status gvrt_read_enclosing(gvrt_handle h, float* density12, float* sh48, fl
  * quality build of a static scene, VulkanFullRT.cpp:621), 3 the same binned SAH on the host (the
  * device build's checker: identical trees).  collapse: 0 greedy surface-area 4-wide collapse on the
  * device, 1 surface-area-optimal collapse (dynamic programming; on the device with builder 2, on
- * the host otherwise). */
+ * the host otherwise).  Every build fits the render kernel's traversal stack, whatever the geometry:
+ * the SAH builds keep a binary depth budget by construction (a split whose larger side could not
+ * finish within it halves the Morton-ordered range instead), and an LBVH or PLOC tree too deep for the
+ * stack is rebuilt by the device SAH build (the Vulkan driver's BVH never refuses a scene either).
+ * depth_budget: 0 = the default budget (43 binary levels, i.e. at most 42 4-wide levels); smaller values
+ * (>= 1 + ceil(log2 survivors)) tighten it for tests of the budget path. */
 typedef struct {
     uint32_t split_cells;
     uint32_t builder;
     uint32_t collapse;
-    uint32_t reserved[5];
+    uint32_t depth_budget;
+    uint32_t reserved[4];
 } gvrt_accel_params;
 
 void gvrt_default_accel_params(gvrt_accel_params* p);
