@@ -407,7 +407,7 @@ __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlan
         float hk_leaf = 0.0f;                                                                                      \
         const RenderRec rec =                                                                                      \
             ADAPTIVE ? load_rec_hk_at(recw, a.leaf_hk, unii(li), hk_leaf) : load_rec_at(recw, unii(li));           \
-        if constexpr (ADAPTIVE) hk_leaf = to_vgpr(hk_leaf);                                                        \
+                                                                                                                   \
         /* split (SplitBLAS analogue): the piece's proxy id and cell; cell == ~0u admits every crossing */         \
         uint4 pa = make_uint4((uint32_t)li, 0xFFFFFFFFu, 0u, 0u);                                                  \
         if (aux_) pa = aux_[li];                                                                                   \
@@ -1036,7 +1036,7 @@ gvrt_status gvrt_launch_render_mode(gvrt_context* c, const RenderArgs& a, uint64
         if (adaptive) GVRT_LAUNCH(false, true, K_HITS, false);
         else GVRT_LAUNCH(false, false, K_HITS, false);
     } else if (adaptive) {
-        GVRT_LAUNCH(false, true, 24, true);  // adaptive leaves at K = 32 spilled 8 B/lane
+        GVRT_LAUNCH(false, true, K_FAST_DEFAULT, true);  // adaptive leaves at the default depth (round 6)
     } else {
         // FAST: the k-buffer depth sets the number of traversal rounds; it can also move rays whose tie or threshold
         // decisions the oracle flags (a round boundary falls elsewhere), so the 24 -> 32 default change altered

@@ -260,7 +260,7 @@ int main(int argc, char** argv) {
                 const auto layout = by_views ? gvrt_host::SplitFrame::VIEWS
                                     : lay == "blocks" ? gvrt_host::SplitFrame::BLOCKS
                                                       : gvrt_host::SplitFrame::COST_BANDS;
-                gvrt_host::SplitFrame sf(app, rank, world, id, W, H, layout, by_views ? &rig : nullptr,
+                gvrt_host::RcclSplitFrame sf(app, rank, world, id, W, H, layout, by_views ? &rig : nullptr,
                                          by_views ? &rig_pi : nullptr);
                 if (sf.status() != GVRT_OK) throw std::runtime_error("SplitFrame: " + sf.error());
                 if (sf.draw(frame) != GVRT_OK || sf.sync() != GVRT_OK) throw std::runtime_error(sf.error());  // warm-up

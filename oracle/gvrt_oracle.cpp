@@ -276,8 +276,10 @@ struct RayState {
     float depth;
 };
 
+// flip (parity accounting, marchRay's alternatives): the accept test taken the other way
 bool processHit(const Scene& s, V3 o, V3 d, uint32_t idx, float minKernelDensity, float minAlpha,
-                uint32_t sphEvalDegree, RayState& st, HitEval* eval = nullptr, float* radmax = nullptr) {
+                uint32_t sphEvalDegree, RayState& st, HitEval* eval = nullptr, float* radmax = nullptr,
+                bool flip = false) {
     const float* rec = s.density + 12ull * idx;
     const V3 pos = v3(rec[0], rec[1], rec[2]);
     const float dens = rec[3];
@@ -295,7 +297,7 @@ bool processHit(const Scene& s, V3 o, V3 d, uint32_t idx, float minKernelDensity
     const float grayDist = dot(gcrod, gcrod);
     const float gres = particleResponse(grayDist);
     const float galpha = std::min(0.99f, gres * dens);
-    const bool acceptHit = (gres > minKernelDensity) && (galpha > minAlpha);
+    const bool acceptHit = flip != ((gres > minKernelDensity) && (galpha > minAlpha));
     if (eval) *eval = HitEval{gres, galpha, responseCond(grayDist, length(gro))};
     if (acceptHit) {
         const float weight = galpha * st.T;
@@ -712,16 +714,82 @@ static void genRay(const float* viewInv, const float* projInv, uint32_t x, uint3
 struct Hit {
     uint32_t id;
     float t;
-    float kt = 0.0f;  // parity accounting: relative change of t per ulp of rounding (icosaCross); 0 for triangles
+    float kt = 0.0f;   // parity accounting: relative change of t per ulp of rounding (icosaCross); 0 for triangles
+    uint8_t face = 0;  // which crossing of the proxy: 0 entry, 1 exit (triangle soup: 0)
 };
 
 // debugging aid: when set (single-threaded trace of one ray), every processed crossing is appended as
 // {id, t, gres, galpha, T after, accepted, round}
 static thread_local std::vector<float>* g_trace = nullptr;
 
+// ---- Alternative outcomes of flagged decisions (parity accounting only).  Every decision the margins
+// flag can go the other way under another float evaluation of the ray (the GPU's).  The march records, for each
+// flagged decision, the variants that other outcome can take (one decision may have several: a near-tied pair may
+// swap or, tied bitwise at a round boundary of the other evaluation, lose either crossing to the exclusive tmin, Q13),
+// each a change to one crossing or one particle:
+//   VAR_ACCEPT  the particle's accept test (response vs hitMinGaussianResponse, alpha vs alphaMin) inverted, for every
+//               crossing of it (gaussianfunctions.glsl:192-200; both faces share the response);
+//   VAR_TERM    the transmittance test after crossing (id, face): mode 0 the ray stops there (T <= minTransmittance),
+//               mode 1 it goes on until its next accepted crossing (particleRendering.comp:153-187);
+//   VAR_SET_T   crossing (id, face) found at t instead (a near tie resolved the other way: it moves just past its
+//               neighbour, or to `last`);
+//   VAR_DROP    crossing (id, face) dropped (its t tied bitwise with `last` at a round boundary, Q13);
+//   VAR_GRAZE   the proxy's crossing pair toggled (a grazing ray: crossed or not is a few-ulp decision).
+// A re-march with a set of variants applied (Forced) gives that alternative's colour.
+enum : uint8_t { VAR_ACCEPT = 1, VAR_TERM = 2, VAR_SET_T = 3, VAR_DROP = 4, VAR_GRAZE = 5 };
+struct Variant {
+    uint8_t kind, face, mode;
+    uint32_t id;
+    float t;
+    uint32_t group;  // the flagged decision it belongs to (variants of one decision are exclusive)
+};
+struct Forced {
+    const Variant* v = nullptr;
+    int n = 0;
+    bool accept_flip(uint32_t id) const {
+        bool f = false;
+        for (int i = 0; i < n; ++i) f ^= v[i].kind == VAR_ACCEPT && v[i].id == id;
+        return f;
+    }
+    bool graze(uint32_t id) const {
+        for (int i = 0; i < n; ++i)
+            if (v[i].kind == VAR_GRAZE && v[i].id == id) return true;
+        return false;
+    }
+    // the crossing's t in this alternative; false: dropped
+    bool crossing(uint32_t id, uint8_t face, float& t) const {
+        for (int i = 0; i < n; ++i) {
+            if (v[i].id != id || v[i].face != face) continue;
+            if (v[i].kind == VAR_DROP) return false;
+            if (v[i].kind == VAR_SET_T) t = v[i].t;
+        }
+        return true;
+    }
+    int term(uint32_t id, uint8_t face) const {  // -1: none, else the mode
+        for (int i = 0; i < n; ++i)
+            if (v[i].kind == VAR_TERM && v[i].id == id && v[i].face == face) return v[i].mode;
+        return -1;
+    }
+};
+
+struct OracleScene {
+    Scene s;
+    Bvh bvh;
+    uint32_t proxy_mode;
+};
+
+struct RayOut {
+    float rgba[4];
+    float depth;
+    uint32_t stats[3];
+    float margin[4];
+};
+
+}  // extern "C"
+
 // The per-ray ray-march: particleRendering.comp:117-191 (RQ) / raygen.rgen:113-193 (RT).
-// out_stats[3*r] = processed crossings (X_r), [3r+1] = accepted (A_r), [3r+2] = rounds.
-// out_margin[4*r .. 4*r+3] (optional; parity accounting, not part of the reference algorithm): how
+// out.stats = {processed crossings (X_r), accepted (A_r), rounds}.
+// out.margin (want_margin; parity accounting, not part of the reference algorithm): how
 // close the ray came to a decision that a few-ulp different float evaluation (GPU exp / rsqrt / rcp,
 // FMA contraction) could take the other way.  Columns 0-2 are normalised to their fixed epsilon: a distance r
 // against the decision's uncertainty max(eps, flag_cond_ulps x its conditioning) is stored as r x eps /
@@ -745,11 +813,347 @@ static thread_local std::vector<float>* g_trace = nullptr;
 //       the sum over the ray's flagged crossings (both of a flagged pair) of 2 T_j a_j, plus minTransmittance / (1 -
 //       the largest such a_j), times c, the largest radiance channel of every crossing composited or flagged on the
 //       ray.  0 for a ray with no flagged decision.
-struct OracleScene {
-    Scene s;
-    Bvh bvh;
-    uint32_t proxy_mode;
-};
+// F (alternatives): the flagged decisions' variants to apply; rec: where the flagged decisions' variants are recorded
+// (with want_margin).
+static void marchRay(const OracleScene& os, const oracle_params* P, V3 o, V3 d, bool want_margin, const Forced* F,
+                     std::vector<Variant>* rec, RayOut& out) {
+    const Scene& s = os.s;
+    const Bvh& bvh = os.bvh;
+    const float* verts = s.verts;
+    const uint32_t* tris = s.tris;
+    const float CU = P->flag_cond_ulps >= 0.0f ? P->flag_cond_ulps : FLAG_COND_ULPS;
+    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    RayState st;
+    st.T = 1.0f;
+    st.rad[0] = st.rad[1] = st.rad[2] = 0.0f;
+    st.rad[3] = P->alpha_init;
+    st.depth = 0.0f;
+    uint32_t nproc = 0, nacc = 0, rounds = 0;
+    float tminb, tmaxb;
+    intersectAABB(P->aabb, o, d, tminb, tmaxb);
+    float last = std::max(0.0f, tminb - EPS_T);
+    Hit kb[MAX_HIT_PER_TRACE];
+    float m_thr = INFINITY, m_t = INFINITY, m_b = INFINITY, prev_t = NAN, prev_acc_t = NAN;
+    // t conditioning of the previous processed / accepted crossing, and the relative uncertainty of T (the summed
+    // relative errors of its factors 1 - alpha_j: alpha_j / (1 - alpha_j) x FLAG_COND_ULPS x cond_j, plus one
+    // rounding per factor)
+    float prev_kt = 0.0f, prev_acc_kt = 0.0f, t_unc = 0.0f;
+    // flip bound (margin[3]): summed T x alpha of the flagged decisions, the largest radiance channel
+    // involved, and the previous accepted crossing's T before it and alpha (pair swaps)
+    float fw = 0.0f, fc = 0.0f, famax = 0.0f, prev_acc_T = 0.0f, prev_acc_a = 0.0f;
+    bool flagged = false;
+    uint32_t prev_id_acc = INVALID_PARTICLE_ID;
+    uint8_t prev_face = 0, prev_acc_face = 0;
+    uint32_t group = 0;  // flagged decisions recorded so far (rec)
+    // a crossing `id` that a flagged decision may add or drop, with T before it and its alpha
+    auto flag = [&](float T, float alpha, uint32_t id) {
+        flagged = true;
+        fw += 2.0f * T * alpha;
+        famax = std::max(famax, alpha);
+        if (id != INVALID_PARTICLE_ID) fc = std::max(fc, radianceMax(s, id, d, P->sph_eval_degree));
+    };
+    // the variants of one flagged decision (rec)
+    auto record = [&](std::initializer_list<Variant> vs) {
+        if (!rec) return;
+        for (Variant v : vs) {
+            v.group = group;
+            rec->push_back(v);
+        }
+        ++group;
+    };
+    // the alternative's accept test of particle id
+    auto acceptOf = [&](uint32_t id, bool a) { return F && F->accept_flip(id) ? !a : a; };
+    // the ray is composited on while T > minTransmittance; an alternative may stop it after a crossing, or carry it
+    // past one up to its next accepted crossing
+    bool forced_stop = false, forced_go = false;
+    auto alive = [&]() { return !forced_stop && (forced_go || st.T > P->min_transmittance); };
+    bool round_start = false;
+    uint32_t prev_id = INVALID_PARTICLE_ID;
+    std::vector<uint32_t> last_ids;  // ids processed with t == last (tie detection, margin)
+    std::vector<uint32_t> stack;
+    stack.reserve(128);
+    while (last <= tmaxb && alive()) {
+        if (P->max_rounds && rounds >= P->max_rounds) break;
+        ++rounds;
+        const float tmin = last + EPS_T, tmax = tmaxb + EPS_T;
+        const float T_round = st.T;
+        for (uint32_t i = 0; i < MAX_HIT_PER_TRACE; ++i) kb[i] = Hit{INVALID_PARTICLE_ID, INFINITE_DISTANCE};
+        Hit h_out{INVALID_PARTICLE_ID, INFINITE_DISTANCE};  // nearest crossing left out of a full buffer
+        // ---- trace(): driver traversal + any-hit (anyhit.rahit:40-71)
+        auto anyhit = [&](uint32_t pid, float t, float kt, uint8_t face) {
+            if (F && !F->crossing(pid, face, t)) return;
+            const bool inRange = (P->tmin_inclusive ? t >= tmin : t > tmin) && t <= tmax;
+            if (!inRange) {
+                if (want_margin && t == last && t <= tmax &&
+                    std::find(last_ids.begin(), last_ids.end(), pid) == last_ids.end()) {
+                    m_b = 0.0f;  // dropped only because its t ties with the last processed crossing
+                    const HitEval he = evalResponse(s, pid, o, d);
+                    if (he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min) {
+                        flag(T_round, he.galpha, pid);
+                        // the other evaluation finds it just past `last`
+                        record({Variant{VAR_SET_T, face, 0, pid, std::nextafter(last, INFINITY), 0}});
+                    }
+                }
+                return;
+            }
+            if (P->drop_rejected) {
+                const HitEval he = evalResponse(s, pid, o, d);
+                if (!acceptOf(pid, he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min)) return;
+            }
+            Hit hit{pid, t, kt, face};
+            if (hit.t < kb[MAX_HIT_PER_TRACE - 1].t) {
+                for (uint32_t i = 0; i < MAX_HIT_PER_TRACE; ++i) {  // compareAndSwapHitPayloadValue
+                    if (hit.t < kb[i].t) std::swap(hit, kb[i]);
+                }
+            }
+            // margin: the nearest crossing left out of (or pushed out of) the full buffer
+            if (hit.id != INVALID_PARTICLE_ID && hit.t < h_out.t) h_out = hit;
+        };
+        stack.clear();
+        stack.push_back(0);
+        while (!stack.empty()) {
+            const uint32_t ni = stack.back();
+            stack.pop_back();
+            const BNode& nd = bvh.nodes[ni];
+            const float tcull = kb[MAX_HIT_PER_TRACE - 1].t < INFINITE_DISTANCE
+                                    ? std::min(tmax, kb[MAX_HIT_PER_TRACE - 1].t)
+                                    : tmax;
+            if (!boxHit(nd, o, inv, tmin, tcull)) continue;
+            if (nd.count == 0) {
+                // front-to-back: pop the nearer child first (culling only; results unchanged)
+                float e0 = INFINITY, e1 = INFINITY;
+                const bool h0 = boxHit(bvh.nodes[nd.left], o, inv, tmin, tcull, &e0);
+                const bool h1 = boxHit(bvh.nodes[nd.left + 1], o, inv, tmin, tcull, &e1);
+                if (h0 && h1) {
+                    stack.push_back(e0 <= e1 ? nd.left + 1 : nd.left);
+                    stack.push_back(e0 <= e1 ? nd.left : nd.left + 1);
+                } else if (h0) {
+                    stack.push_back(nd.left);
+                } else if (h1) {
+                    stack.push_back(nd.left + 1);
+                }
+                continue;
+            }
+            for (uint32_t k = 0; k < nd.count; ++k) {
+                const uint32_t g = bvh.items[nd.left + k];
+                if (P->proxy_mode == 1) {
+                    float tin, tout, kin = 0.0f, kout = 0.0f;
+                    bool crossed = icosaCross(s, g, o, d, tin, tout, &kin, &kout);
+                    const float geps = std::max(FLAG_BOUND_EPS, CU * (kin + kout));
+                    if (want_margin && std::fabs(tout - tin) < geps * std::max(std::fabs(tin), std::fabs(tout))) {
+                        // grazing the proxy: whether it is crossed at all is a few-ulp decision; it
+                        // matters when its crossings would be composited
+                        const HitEval he = evalResponse(s, g, o, d);
+                        if (he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min) {
+                            const float gg = std::fabs(tout - tin) / std::max(std::fabs(tin), 1e-30f);
+                            m_b = std::min(m_b, normMargin(gg, FLAG_BOUND_EPS, geps));
+                            if (gg < geps) {  // both crossings of the proxy
+                                flag(T_round, he.galpha, g);
+                                flag(T_round, he.galpha, g);
+                                record({Variant{VAR_GRAZE, 0, 0, g, 0.0f, 0}});
+                            }
+                        }
+                    }
+                    if (F && F->graze(g)) {  // the other evaluation crosses it, or misses it
+                        if (crossed) {
+                            crossed = false;
+                        } else if (std::fabs(tout - tin) < geps * std::max(std::fabs(tin), std::fabs(tout))) {
+                            crossed = true;
+                            const float a = std::min(tin, tout), b = std::max(tin, tout);
+                            tin = a;
+                            tout = b;
+                        }
+                    }
+                    if (crossed) {
+                        anyhit(g, tin, kin, 0);
+                        anyhit(g, tout, kout, 1);
+                    }
+                } else {
+                    // watertight setup
+                    int kz = 0;
+                    float ax = std::fabs(d.x), ay = std::fabs(d.y), az = std::fabs(d.z);
+                    if (ay > ax && ay >= az) kz = 1;
+                    else if (az > ax && az > ay) kz = 2;
+                    int kx = (kz + 1) % 3, ky = (kx + 1) % 3;
+                    if (comp(d, kz) < 0.0f) std::swap(kx, ky);
+                    const float Sx = comp(d, kx) / comp(d, kz), Sy = comp(d, ky) / comp(d, kz),
+                                Sz = 1.0f / comp(d, kz);
+                    for (uint32_t t = 0; t < 20; ++t) {
+                        const uint32_t* tr = tris + 60ull * g + 3 * t;
+                        const V3 p0 = v3(verts[3ull * tr[0]], verts[3ull * tr[0] + 1], verts[3ull * tr[0] + 2]);
+                        const V3 p1 = v3(verts[3ull * tr[1]], verts[3ull * tr[1] + 1], verts[3ull * tr[1] + 2]);
+                        const V3 p2 = v3(verts[3ull * tr[2]], verts[3ull * tr[2] + 1], verts[3ull * tr[2] + 2]);
+                        float th;
+                        if (rayTri(o, d, kx, ky, kz, Sx, Sy, Sz, p0, p1, p2, th))
+                            anyhit((20 * g + t) / 20, th, 0.0f, 0);  // Q2: particle id = primitive / 20
+                    }
+                }
+            }
+        }
+        if (kb[0].id == INVALID_PARTICLE_ID) break;
+        auto gap = [](float a, float b) { return std::fabs(a - b) / std::max(std::fabs(a), 1e-30f); };
+        // margin: a crossing tied with the buffer's last slot may or may not make this round,
+        // depending on arrival order
+        auto accepted = [&](uint32_t id) {
+            const HitEval he = evalResponse(s, id, o, d);
+            return he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min;
+        };
+        // (which of two tied crossings makes the round changes the image only if one of them is accepted)
+        // (the uncertainty of a gap between two crossings: the larger of the fixed epsilon and their summed
+        // t conditioning)
+        auto teps = [CU](float eps, const Hit& a, const Hit& b) { return std::max(eps, CU * (a.kt + b.kt)); };
+        const Hit& k15 = kb[MAX_HIT_PER_TRACE - 1];
+        if (want_margin && k15.id != INVALID_PARTICLE_ID && h_out.id != INVALID_PARTICLE_ID &&
+            gap(k15.t, h_out.t) < teps(FLAG_BOUND_EPS, k15, h_out) && (accepted(k15.id) || accepted(h_out.id))) {
+            const float gg = gap(k15.t, h_out.t);
+            const float ge = teps(FLAG_BOUND_EPS, k15, h_out);
+            m_b = std::min(m_b, normMargin(gg, FLAG_BOUND_EPS, ge));
+            if (gg < ge) {
+                flag(T_round, evalResponse(s, k15.id, o, d).galpha, k15.id);
+                flag(T_round, evalResponse(s, h_out.id, o, d).galpha, h_out.id);
+                // the other evaluation takes the crossing left out into this round instead
+                record({Variant{VAR_SET_T, h_out.face, 0, h_out.id, std::nextafter(k15.t, -INFINITY), 0}});
+            }
+        }
+        round_start = true;
+        // ---- process k hits
+        for (uint32_t i = 0; i < MAX_HIT_PER_TRACE; ++i) {
+            const Hit h = kb[i];
+            if (h.id != INVALID_PARTICLE_ID && alive()) {
+                HitEval ev{0.0f, 0.0f};
+                const float T_before = st.T;
+                const bool acc = processHit(s, o, d, h.id, P->hit_min_gaussian_response, P->alpha_min,
+                                            P->sph_eval_degree, st, &ev, want_margin ? &fc : nullptr,
+                                            F && F->accept_flip(h.id));
+                if (acc && forced_go) forced_go = false;  // carried past the stop to this crossing: it is the last
+                if (acc && F) {
+                    const int tm = F->term(h.id, h.face);
+                    if (tm == 0) forced_stop = true;
+                    if (tm == 1 && !(st.T > P->min_transmittance)) forced_go = true;
+                }
+                if (g_trace)
+                    g_trace->insert(g_trace->end(), {(float)h.id, h.t, ev.gres, ev.galpha, st.T, acc ? 1.0f : 0.0f,
+                                                     (float)rounds});
+                if (want_margin) {
+                    const float r0 = std::fabs(ev.gres / P->hit_min_gaussian_response - 1.0f);
+                    const float r1 = std::fabs(ev.galpha / P->alpha_min - 1.0f);
+                    // both thresholds see gres's relative error (galpha = gres x density below the 0.99 clamp)
+                    const float re = std::max(FLAG_THR_EPS, CU * ev.cond);
+                    m_thr = std::min(m_thr, normMargin(std::min(r0, r1), FLAG_THR_EPS, re));
+                    if (r0 < re || r1 < re) {
+                        flag(T_before, ev.galpha, h.id);
+                        record({Variant{VAR_ACCEPT, 0, 0, h.id, 0.0f, 0}});
+                    }
+                    if (acc) {
+                        if (ev.galpha < 0.99f)
+                            t_unc += ev.galpha / (1.0f - ev.galpha) * CU * ev.cond + (CU > 0.0f ? 2.0f * ULP : 0.0f);
+                        const float r2 = std::fabs(st.T / P->min_transmittance - 1.0f);
+                        const float te = std::max(FLAG_THR_EPS, t_unc);
+                        m_thr = std::min(m_thr, normMargin(r2, FLAG_THR_EPS, te));
+                        if (r2 < te) {  // the ray may go on (or stop before this crossing)
+                            const Hit nx = i + 1 < MAX_HIT_PER_TRACE ? kb[i + 1] : h_out;
+                            flag(T_before, ev.galpha, h.id);
+                            flag(st.T, 1.0f, nx.id);
+                            record({Variant{VAR_TERM, h.face, (uint8_t)(st.T > P->min_transmittance ? 0 : 1), h.id,
+                                            0.0f, 0}});
+                        }
+                    }
+                    // (an inclusive tmin re-finds the same crossing: not an ordering question)
+                    const bool refound = h.id == prev_id && h.t == prev_t;
+                    if (acc && round_start && prev_t == prev_t && !refound) {
+                        const float gg = gap(h.t, prev_t);
+                        const float ge = std::max(FLAG_BOUND_EPS, CU * (h.kt + prev_kt));
+                        m_b = std::min(m_b, normMargin(gg, FLAG_BOUND_EPS, ge));
+                        if (gg < ge) {
+                            flag(T_before, ev.galpha, h.id);
+                            // tied with `last` in the other evaluation: one of the two lost to the exclusive tmin
+                            record({Variant{VAR_DROP, h.face, 0, h.id, 0.0f, 0},
+                                    Variant{VAR_DROP, prev_face, 0, prev_id, 0.0f, 0}});
+                        }
+                    }
+                    if (acc && prev_acc_t == prev_acc_t && !refound) {
+                        const float gg = gap(h.t, prev_acc_t);
+                        const float ge = std::max(FLAG_PAIR_EPS, CU * (h.kt + prev_acc_kt));
+                        m_t = std::min(m_t, normMargin(gg, FLAG_PAIR_EPS, ge));
+                        if (gg < ge) {  // may swap, or tie and lose one at a round boundary
+                            flag(prev_acc_T, prev_acc_a, prev_id_acc);
+                            flag(T_before, ev.galpha, h.id);
+                            record({Variant{VAR_SET_T, h.face, 0, h.id, std::nextafter(prev_acc_t, -INFINITY), 0},
+                                    Variant{VAR_DROP, h.face, 0, h.id, 0.0f, 0},
+                                    Variant{VAR_DROP, prev_acc_face, 0, prev_id_acc, 0.0f, 0}});
+                        }
+                    }
+                    round_start = false;
+                    prev_t = h.t;
+                    prev_kt = h.kt;
+                    prev_id = h.id;
+                    prev_face = h.face;
+                    if (acc) {
+                        prev_acc_t = h.t;
+                        prev_acc_kt = h.kt;
+                        prev_acc_T = T_before;
+                        prev_acc_a = ev.galpha;
+                        prev_id_acc = h.id;
+                        prev_acc_face = h.face;
+                    }
+                    if (h.t > last) last_ids.clear();
+                    if (h.t >= last) last_ids.push_back(h.id);
+                    // the crossing that ends the ray against its successor: a tie decides which of
+                    // the two is composited
+                    // (only an accepted successor changes the image by coming first)
+                    if (acc && !(st.T > P->min_transmittance)) {
+                        const Hit nx = i + 1 < MAX_HIT_PER_TRACE && kb[i + 1].id != INVALID_PARTICLE_ID ? kb[i + 1]
+                                                                                                      : h_out;
+                        if (nx.id != INVALID_PARTICLE_ID && gap(h.t, nx.t) < teps(FLAG_BOUND_EPS, h, nx) &&
+                            accepted(nx.id)) {
+                            const float gg = gap(h.t, nx.t);
+                            const float ge = teps(FLAG_BOUND_EPS, h, nx);
+                            m_b = std::min(m_b, normMargin(gg, FLAG_BOUND_EPS, ge));
+                            if (gg < ge) {
+                                flag(T_before, ev.galpha, h.id);
+                                flag(T_before, evalResponse(s, nx.id, o, d).galpha, nx.id);
+                                record({Variant{VAR_SET_T, nx.face, 0, nx.id, std::nextafter(h.t, -INFINITY), 0}});
+                            }
+                        }
+                    }
+                }
+                last = std::max(last, h.t);
+                ++nproc;
+                nacc += acc ? 1 : 0;
+            }
+        }
+    }
+    for (int k = 0; k < 4; ++k) out.rgba[k] = st.rad[k];
+    out.depth = st.depth;
+    out.stats[0] = nproc;
+    out.stats[1] = nacc;
+    out.stats[2] = rounds;
+    out.margin[0] = m_thr;
+    out.margin[1] = m_t;
+    out.margin[2] = m_b;
+    out.margin[3] = flagged ? (fw + P->min_transmittance / std::max(1.0f - famax, 0.01f)) * fc : 0.0f;
+}
+
+// ray r of a launch: its origin and direction (with the parity accounting's perturbation, if any)
+static void rayOf(const oracle_params* P, const float* viewInverse, const float* projInverse, uint32_t W, uint32_t H,
+                  uint64_t r, V3& o, V3& d, uint32_t* cam_out = nullptr, uint32_t* px_out = nullptr,
+                  uint32_t* py_out = nullptr) {
+    const uint32_t cam = (uint32_t)(r / ((uint64_t)W * H));
+    const uint32_t rem = (uint32_t)(r % ((uint64_t)W * H));
+    const uint32_t py = rem / W, px = rem % W;
+    genRay(viewInverse + 16ull * cam, projInverse, px, py, W, H, P->pixel_offset, o, d);
+    g_jig_ulps = P->perturb_ulps;
+    g_jig_ray = r;
+    if (g_jig_ulps) {
+        uint64_t hh = mix64(r + 0x1234567ull);
+        d = jig3(d, hh);
+    }
+    if (cam_out) *cam_out = cam;
+    if (px_out) *px_out = px;
+    if (py_out) *py_out = py;
+}
+
+extern "C" {
 
 // Acceleration structure of the oracle (the driver BLAS/TLAS build is not restated; any
 // correct BVH yields the same k-nearest sets).  Input arrays must outlive the scene.
@@ -815,31 +1219,17 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
     OracleScene* os = static_cast<OracleScene*>(h);
     if (!os || !P || !viewInverse || !projInverse || !out_rgba) return -1;
     if (P->proxy_mode != os->proxy_mode) return -2;
-    const Scene& s = os->s;
-    const Bvh& bvh = os->bvh;
-    const float* verts = s.verts;
-    const uint32_t* tris = s.tris;
-
     const uint64_t nrays_full = (uint64_t)W * H * ncams;
     const uint64_t nwork = subset ? nsubset : nrays_full;
-    const float CU = P->flag_cond_ulps >= 0.0f ? P->flag_cond_ulps : FLAG_COND_ULPS;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #pragma omp parallel for schedule(dynamic, 64)
 #endif
     for (int64_t w = 0; w < (int64_t)nwork; ++w) {
         const uint64_t r = subset ? subset[w] : (uint64_t)w;
-        const uint32_t cam = (uint32_t)(r / ((uint64_t)W * H));
-        const uint32_t rem = (uint32_t)(r % ((uint64_t)W * H));
-        const uint32_t py = rem / W, px = rem % W;
         V3 o, d;
-        genRay(viewInverse + 16ull * cam, projInverse, px, py, W, H, P->pixel_offset, o, d);
-        g_jig_ulps = P->perturb_ulps;
-        g_jig_ray = r;
-        if (g_jig_ulps) {
-            uint64_t h = mix64(r + 0x1234567ull);
-            d = jig3(d, h);
-        }
+        uint32_t cam, px, py;
+        rayOf(P, viewInverse, projInverse, W, H, r, o, d, &cam, &px, &py);
         if (out_ray_dirs) {
             uint64_t di = P->ray_dirs_layout == 1 ? ((uint64_t)cam * W * H + (uint64_t)px * H + py) : r;
             if (subset) di = w;
@@ -848,266 +1238,80 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
             out_ray_dirs[4 * di + 2] = d.z;
             out_ray_dirs[4 * di + 3] = 0.0f;
         }
-        const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-        RayState st;
-        st.T = 1.0f;
-        st.rad[0] = st.rad[1] = st.rad[2] = 0.0f;
-        st.rad[3] = P->alpha_init;
-        st.depth = 0.0f;
-        uint32_t nproc = 0, nacc = 0, rounds = 0;
-        float tminb, tmaxb;
-        intersectAABB(P->aabb, o, d, tminb, tmaxb);
-        float last = std::max(0.0f, tminb - EPS_T);
-        Hit kb[MAX_HIT_PER_TRACE];
-        float m_thr = INFINITY, m_t = INFINITY, m_b = INFINITY, prev_t = NAN, prev_acc_t = NAN;
-        // t conditioning of the previous processed / accepted crossing, and the relative uncertainty of T (the summed
-        // relative errors of its factors 1 - alpha_j: alpha_j / (1 - alpha_j) x FLAG_COND_ULPS x cond_j, plus one
-        // rounding per factor)
-        float prev_kt = 0.0f, prev_acc_kt = 0.0f, t_unc = 0.0f;
-        // flip bound (out_margin[3]): summed T x alpha of the flagged decisions, the largest radiance channel
-        // involved, and the previous accepted crossing's T before it and alpha (pair swaps)
-        float fw = 0.0f, fc = 0.0f, famax = 0.0f, prev_acc_T = 0.0f, prev_acc_a = 0.0f;
-        bool flagged = false;
-        uint32_t prev_id_acc = INVALID_PARTICLE_ID;
-        // a crossing `id` that a flagged decision may add or drop, with T before it and its alpha
-        auto flag = [&](float T, float alpha, uint32_t id) {
-            flagged = true;
-            fw += 2.0f * T * alpha;
-            famax = std::max(famax, alpha);
-            if (id != INVALID_PARTICLE_ID) fc = std::max(fc, radianceMax(s, id, d, P->sph_eval_degree));
-        };
-        bool round_start = false;
-        uint32_t prev_id = INVALID_PARTICLE_ID;
-        std::vector<uint32_t> last_ids;  // ids processed with t == last (tie detection, out_margin)
-        std::vector<uint32_t> stack;
-        stack.reserve(128);
-        while (last <= tmaxb && st.T > P->min_transmittance) {
-            if (P->max_rounds && rounds >= P->max_rounds) break;
-            ++rounds;
-            const float tmin = last + EPS_T, tmax = tmaxb + EPS_T;
-            const float T_round = st.T;
-            for (uint32_t i = 0; i < MAX_HIT_PER_TRACE; ++i) kb[i] = Hit{INVALID_PARTICLE_ID, INFINITE_DISTANCE};
-            Hit h_out{INVALID_PARTICLE_ID, INFINITE_DISTANCE};  // nearest crossing left out of a full buffer
-            // ---- trace(): driver traversal + any-hit (anyhit.rahit:40-71)
-            auto anyhit = [&](uint32_t pid, float t, float kt) {
-                const bool inRange = (P->tmin_inclusive ? t >= tmin : t > tmin) && t <= tmax;
-                if (!inRange) {
-                    if (out_margin && t == last && t <= tmax &&
-                        std::find(last_ids.begin(), last_ids.end(), pid) == last_ids.end()) {
-                        m_b = 0.0f;  // dropped only because its t ties with the last processed crossing
-                        const HitEval he = evalResponse(s, pid, o, d);
-                        if (he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min)
-                            flag(T_round, he.galpha, pid);
-                    }
-                    return;
-                }
-                if (P->drop_rejected) {
-                    const HitEval he = evalResponse(s, pid, o, d);
-                    if (!(he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min)) return;
-                }
-                Hit hit{pid, t, kt};
-                if (hit.t < kb[MAX_HIT_PER_TRACE - 1].t) {
-                    for (uint32_t i = 0; i < MAX_HIT_PER_TRACE; ++i) {  // compareAndSwapHitPayloadValue
-                        if (hit.t < kb[i].t) std::swap(hit, kb[i]);
-                    }
-                }
-                // out_margin: the nearest crossing left out of (or pushed out of) the full buffer
-                if (hit.id != INVALID_PARTICLE_ID && hit.t < h_out.t) h_out = hit;
-            };
-            stack.clear();
-            stack.push_back(0);
-            while (!stack.empty()) {
-                const uint32_t ni = stack.back();
-                stack.pop_back();
-                const BNode& nd = bvh.nodes[ni];
-                const float tcull = kb[MAX_HIT_PER_TRACE - 1].t < INFINITE_DISTANCE
-                                        ? std::min(tmax, kb[MAX_HIT_PER_TRACE - 1].t)
-                                        : tmax;
-                if (!boxHit(nd, o, inv, tmin, tcull)) continue;
-                if (nd.count == 0) {
-                    // front-to-back: pop the nearer child first (culling only; results unchanged)
-                    float e0 = INFINITY, e1 = INFINITY;
-                    const bool h0 = boxHit(bvh.nodes[nd.left], o, inv, tmin, tcull, &e0);
-                    const bool h1 = boxHit(bvh.nodes[nd.left + 1], o, inv, tmin, tcull, &e1);
-                    if (h0 && h1) {
-                        stack.push_back(e0 <= e1 ? nd.left + 1 : nd.left);
-                        stack.push_back(e0 <= e1 ? nd.left : nd.left + 1);
-                    } else if (h0) {
-                        stack.push_back(nd.left);
-                    } else if (h1) {
-                        stack.push_back(nd.left + 1);
-                    }
-                    continue;
-                }
-                for (uint32_t k = 0; k < nd.count; ++k) {
-                    const uint32_t g = bvh.items[nd.left + k];
-                    if (P->proxy_mode == 1) {
-                        float tin, tout, kin = 0.0f, kout = 0.0f;
-                        const bool crossed = icosaCross(s, g, o, d, tin, tout, &kin, &kout);
-                        const float geps = std::max(FLAG_BOUND_EPS, CU * (kin + kout));
-                        if (out_margin && std::fabs(tout - tin) < geps * std::max(std::fabs(tin), std::fabs(tout))) {
-                            // grazing the proxy: whether it is crossed at all is a few-ulp decision; it
-                            // matters when its crossings would be composited
-                            const HitEval he = evalResponse(s, g, o, d);
-                            if (he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min) {
-                                const float gg = std::fabs(tout - tin) / std::max(std::fabs(tin), 1e-30f);
-                                m_b = std::min(m_b, normMargin(gg, FLAG_BOUND_EPS, geps));
-                                if (gg < geps) {  // both crossings of the proxy
-                                    flag(T_round, he.galpha, g);
-                                    flag(T_round, he.galpha, g);
-                                }
-                            }
-                        }
-                        if (crossed) {
-                            anyhit(g, tin, kin);
-                            anyhit(g, tout, kout);
-                        }
-                    } else {
-                        // watertight setup
-                        int kz = 0;
-                        float ax = std::fabs(d.x), ay = std::fabs(d.y), az = std::fabs(d.z);
-                        if (ay > ax && ay >= az) kz = 1;
-                        else if (az > ax && az > ay) kz = 2;
-                        int kx = (kz + 1) % 3, ky = (kx + 1) % 3;
-                        if (comp(d, kz) < 0.0f) std::swap(kx, ky);
-                        const float Sx = comp(d, kx) / comp(d, kz), Sy = comp(d, ky) / comp(d, kz),
-                                    Sz = 1.0f / comp(d, kz);
-                        for (uint32_t t = 0; t < 20; ++t) {
-                            const uint32_t* tr = tris + 60ull * g + 3 * t;
-                            const V3 p0 = v3(verts[3ull * tr[0]], verts[3ull * tr[0] + 1], verts[3ull * tr[0] + 2]);
-                            const V3 p1 = v3(verts[3ull * tr[1]], verts[3ull * tr[1] + 1], verts[3ull * tr[1] + 2]);
-                            const V3 p2 = v3(verts[3ull * tr[2]], verts[3ull * tr[2] + 1], verts[3ull * tr[2] + 2]);
-                            float th;
-                            if (rayTri(o, d, kx, ky, kz, Sx, Sy, Sz, p0, p1, p2, th))
-                                anyhit((20 * g + t) / 20, th, 0.0f);  // Q2: particle id = primitive / 20
-                        }
-                    }
-                }
-            }
-            if (kb[0].id == INVALID_PARTICLE_ID) break;
-            auto gap = [](float a, float b) { return std::fabs(a - b) / std::max(std::fabs(a), 1e-30f); };
-            // out_margin: a crossing tied with the buffer's last slot may or may not make this round,
-            // depending on arrival order
-            auto accepted = [&](uint32_t id) {
-                const HitEval he = evalResponse(s, id, o, d);
-                return he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min;
-            };
-            // (which of two tied crossings makes the round changes the image only if one of them is accepted)
-            // (the uncertainty of a gap between two crossings: the larger of the fixed epsilon and their summed
-            // t conditioning)
-            auto teps = [CU](float eps, const Hit& a, const Hit& b) { return std::max(eps, CU * (a.kt + b.kt)); };
-            if (out_margin && kb[MAX_HIT_PER_TRACE - 1].id != INVALID_PARTICLE_ID && h_out.id != INVALID_PARTICLE_ID &&
-                gap(kb[MAX_HIT_PER_TRACE - 1].t, h_out.t) < teps(FLAG_BOUND_EPS, kb[MAX_HIT_PER_TRACE - 1], h_out) &&
-                (accepted(kb[MAX_HIT_PER_TRACE - 1].id) || accepted(h_out.id))) {
-                const float gg = gap(kb[MAX_HIT_PER_TRACE - 1].t, h_out.t);
-                const float ge = teps(FLAG_BOUND_EPS, kb[MAX_HIT_PER_TRACE - 1], h_out);
-                m_b = std::min(m_b, normMargin(gg, FLAG_BOUND_EPS, ge));
-                if (gg < ge) {
-                    flag(T_round, evalResponse(s, kb[MAX_HIT_PER_TRACE - 1].id, o, d).galpha,
-                         kb[MAX_HIT_PER_TRACE - 1].id);
-                    flag(T_round, evalResponse(s, h_out.id, o, d).galpha, h_out.id);
-                }
-            }
-            round_start = true;
-            // ---- process k hits
-            for (uint32_t i = 0; i < MAX_HIT_PER_TRACE; ++i) {
-                const Hit h = kb[i];
-                if (h.id != INVALID_PARTICLE_ID && st.T > P->min_transmittance) {
-                    HitEval ev{0.0f, 0.0f};
-                    const float T_before = st.T;
-                    const bool acc = processHit(s, o, d, h.id, P->hit_min_gaussian_response, P->alpha_min,
-                                                P->sph_eval_degree, st, &ev, out_margin ? &fc : nullptr);
-                    if (g_trace)
-                        g_trace->insert(g_trace->end(), {(float)h.id, h.t, ev.gres, ev.galpha, st.T, acc ? 1.0f : 0.0f,
-                                                         (float)rounds});
-                    if (out_margin) {
-                        const float r0 = std::fabs(ev.gres / P->hit_min_gaussian_response - 1.0f);
-                        const float r1 = std::fabs(ev.galpha / P->alpha_min - 1.0f);
-                        // both thresholds see gres's relative error (galpha = gres x density below the 0.99 clamp)
-                        const float re = std::max(FLAG_THR_EPS, CU * ev.cond);
-                        m_thr = std::min(m_thr, normMargin(std::min(r0, r1), FLAG_THR_EPS, re));
-                        if (r0 < re || r1 < re) flag(T_before, ev.galpha, h.id);
-                        if (acc) {
-                            if (ev.galpha < 0.99f)
-                                t_unc += ev.galpha / (1.0f - ev.galpha) * CU * ev.cond + (CU > 0.0f ? 2.0f * ULP : 0.0f);
-                            const float r2 = std::fabs(st.T / P->min_transmittance - 1.0f);
-                            const float te = std::max(FLAG_THR_EPS, t_unc);
-                            m_thr = std::min(m_thr, normMargin(r2, FLAG_THR_EPS, te));
-                            if (r2 < te) {  // the ray may go on (or stop before this crossing)
-                                const Hit nx = i + 1 < MAX_HIT_PER_TRACE ? kb[i + 1] : h_out;
-                                flag(T_before, ev.galpha, h.id);
-                                flag(st.T, 1.0f, nx.id);
-                            }
-                        }
-                        // (an inclusive tmin re-finds the same crossing: not an ordering question)
-                        const bool refound = h.id == prev_id && h.t == prev_t;
-                        if (acc && round_start && prev_t == prev_t && !refound) {
-                            const float gg = gap(h.t, prev_t);
-                            const float ge = std::max(FLAG_BOUND_EPS, CU * (h.kt + prev_kt));
-                            m_b = std::min(m_b, normMargin(gg, FLAG_BOUND_EPS, ge));
-                            if (gg < ge) flag(T_before, ev.galpha, h.id);
-                        }
-                        if (acc && prev_acc_t == prev_acc_t && !refound) {
-                            const float gg = gap(h.t, prev_acc_t);
-                            const float ge = std::max(FLAG_PAIR_EPS, CU * (h.kt + prev_acc_kt));
-                            m_t = std::min(m_t, normMargin(gg, FLAG_PAIR_EPS, ge));
-                            if (gg < ge) {  // may swap, or tie and lose one at a round boundary
-                                flag(prev_acc_T, prev_acc_a, prev_id_acc);
-                                flag(T_before, ev.galpha, h.id);
-                            }
-                        }
-                        round_start = false;
-                        prev_t = h.t;
-                        prev_kt = h.kt;
-                        prev_id = h.id;
-                        if (acc) {
-                            prev_acc_t = h.t;
-                            prev_acc_kt = h.kt;
-                            prev_acc_T = T_before;
-                            prev_acc_a = ev.galpha;
-                            prev_id_acc = h.id;
-                        }
-                        if (h.t > last) last_ids.clear();
-                        if (h.t >= last) last_ids.push_back(h.id);
-                        // the crossing that ends the ray against its successor: a tie decides which of
-                        // the two is composited
-                        // (only an accepted successor changes the image by coming first)
-                        if (acc && !(st.T > P->min_transmittance)) {
-                            const Hit nx = i + 1 < MAX_HIT_PER_TRACE && kb[i + 1].id != INVALID_PARTICLE_ID ? kb[i + 1]
-                                                                                                          : h_out;
-                            if (nx.id != INVALID_PARTICLE_ID && gap(h.t, nx.t) < teps(FLAG_BOUND_EPS, h, nx) &&
-                                accepted(nx.id)) {
-                                const float gg = gap(h.t, nx.t);
-                                const float ge = teps(FLAG_BOUND_EPS, h, nx);
-                                m_b = std::min(m_b, normMargin(gg, FLAG_BOUND_EPS, ge));
-                                if (gg < ge) {
-                                    flag(T_before, ev.galpha, h.id);
-                                    flag(T_before, evalResponse(s, nx.id, o, d).galpha, nx.id);
-                                }
-                            }
-                        }
-                    }
-                    last = std::max(last, h.t);
-                    ++nproc;
-                    nacc += acc ? 1 : 0;
-                }
-            }
-        }
+        RayOut ro;
+        marchRay(*os, P, o, d, out_margin != nullptr, nullptr, nullptr, ro);
         const uint64_t oi = subset ? (uint64_t)w : r;
-        for (int k = 0; k < 4; ++k) out_rgba[4 * oi + k] = st.rad[k];
-        if (out_depth) out_depth[oi] = st.depth;
-        if (out_stats) {
-            out_stats[3 * oi] = nproc;
-            out_stats[3 * oi + 1] = nacc;
-            out_stats[3 * oi + 2] = rounds;
-        }
-        if (out_margin) {
-            out_margin[4 * oi] = m_thr;
-            out_margin[4 * oi + 1] = m_t;
-            out_margin[4 * oi + 2] = m_b;
-            out_margin[4 * oi + 3] =
-                flagged ? (fw + P->min_transmittance / std::max(1.0f - famax, 0.01f)) * fc : 0.0f;
-        }
+        for (int k = 0; k < 4; ++k) out_rgba[4 * oi + k] = ro.rgba[k];
+        if (out_depth) out_depth[oi] = ro.depth;
+        if (out_stats)
+            for (int k = 0; k < 3; ++k) out_stats[3 * oi + k] = ro.stats[k];
+        if (out_margin)
+            for (int k = 0; k < 4; ++k) out_margin[4 * oi + k] = ro.margin[k];
+    }
+    return 0;
+}
+
+// Explaining a ray's flagged decisions (parity accounting): the ray re-marched with its flagged
+// decisions taken the other way.  For each ray rays[k] the march records every flagged decision's variants
+// (Variant); the alternatives are the base march, each single variant, then each pair of variants of two different
+// decisions (at most max_pairs pairs), tried in that order until one lies within tol of target[3k .. 3k+2] (max
+// |d rgb|).  out[4k ..]: {the distance of the nearest alternative tried, its kind (0 base, 1 single, 2 pair), the
+// number of variants, the number of decisions}.  alt_rgba (optional, 4 floats per ray): that alternative's colour.
+int oracle_scene_explain(void* h, const oracle_params* P, const float* viewInverse, const float* projInverse,
+                         uint32_t W, uint32_t H, uint32_t ncams, const uint64_t* rays, uint64_t n, const float* target,
+                         float tol, uint32_t max_pairs, float* out, float* alt_rgba, int nthreads) {
+    OracleScene* os = static_cast<OracleScene*>(h);
+    if (!os || !P || !viewInverse || !projInverse || !rays || !target || !out) return -1;
+    if (P->proxy_mode != os->proxy_mode) return -2;
+    (void)ncams;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (int64_t k = 0; k < (int64_t)n; ++k) {
+        V3 o, d;
+        rayOf(P, viewInverse, projInverse, W, H, rays[k], o, d);
+        std::vector<Variant> vars;
+        RayOut base;
+        marchRay(*os, P, o, d, true, nullptr, &vars, base);
+        const float* tg = target + 3 * k;
+        auto dist = [&](const RayOut& ro) {
+            float m = 0.0f;
+            for (int c = 0; c < 3; ++c) m = std::max(m, std::fabs(ro.rgba[c] - tg[c]));
+            return m;
+        };
+        float best = dist(base);
+        int kind = 0;
+        RayOut best_out = base;
+        uint32_t ngroups = vars.empty() ? 0u : vars.back().group + 1u;
+        auto consider = [&](const Variant* v, int nv, int knd) {
+            Forced F;
+            F.v = v;
+            F.n = nv;
+            RayOut ro;
+            marchRay(*os, P, o, d, false, &F, nullptr, ro);
+            const float dd = dist(ro);
+            if (dd < best) {
+                best = dd;
+                kind = knd;
+                best_out = ro;
+            }
+        };
+        for (size_t i = 0; i < vars.size() && best > tol; ++i) consider(&vars[i], 1, 1);
+        uint32_t pairs = 0;
+        for (size_t i = 0; i < vars.size() && best > tol && pairs < max_pairs; ++i)
+            for (size_t j = i + 1; j < vars.size() && best > tol && pairs < max_pairs; ++j) {
+                if (vars[i].group == vars[j].group) continue;
+                const Variant two[2] = {vars[i], vars[j]};
+                consider(two, 2, 2);
+                ++pairs;
+            }
+        out[4 * k] = best;
+        out[4 * k + 1] = (float)kind;
+        out[4 * k + 2] = (float)vars.size();
+        out[4 * k + 3] = (float)ngroups;
+        if (alt_rgba)
+            for (int c = 0; c < 4; ++c) alt_rgba[4 * k + c] = best_out.rgba[c];
     }
     return 0;
 }

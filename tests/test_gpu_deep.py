@@ -10,16 +10,15 @@
     build, which is depth-bounded by construction.  The Vulkan driver's BVH it replaces never refuses a scene
     (VulkanFullRT.cpp:575-674).
   * scene.trained_standin (1 M, seed 5: surfels and needles along surfaces, heavy-tailed sizes, 0.1 % giants,
-    bimodal opacity) at 1920x1080 with the bench's build against the oracle on every 4th ray (the oracle spends
-    ~0.7 ms per ray on this scene's ~2.8 k proxy tests, so the whole frame would take ~25 min on the box's 16
-    threads; a strided sample of a per-ray restatement is a valid sample).
+    bimodal opacity) at 1920x1080 with the bench's build against the oracle on every ray of the frame, FAST and
+    LITERAL, every flagged ray that differs explained exactly (explain_flagged).
 """
 import math
 
 import numpy as np
 import pytest
 
-from test_gpu_parity import _cmp_images, parity_figures, record_parity
+from test_gpu_parity import _cmp_images, assert_explained, explain_flagged, parity_figures, record_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -99,17 +98,22 @@ def test_trained_standin_vs_oracle(gv, O):
     print(f"trained stand-in: M {m}, bvh depth {st['bvh_depth']} / 4-wide {st['bvh_depth4']}")
     e = O.enclose(splats)
     assert e["m"] == m
-    sub = np.arange(0, W * H, 4, dtype=np.uint64)
+    sub = np.arange(0, W * H, 1, dtype=np.uint64)  # every ray
     sc = O.Scene(e)
+    idx = sub.astype(np.int64)
     try:
         ref = sc.render(vi, pi, W, H, subset=sub, margin=True)
+        assert (ref["rgba32f"].reshape(-1, 4)[:, 3] > 0).mean() > 0.95
+        _cmp_images(fast["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.0045)  # 0.405 % flagged
+        _cmp_images(lit["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.0045)
+        amb = O.ambiguous(ref["margin"])
+        stats = ref["stats"].reshape(-1, 3)
+        assert (fast["hit_counts"].reshape(-1)[idx] != stats[:, 1])[~amb].sum() == 0
+        ex = explain_flagged(O, sc, vi, pi, W, H, fast["rgba32f"].reshape(-1, 4)[idx], ref, rays=sub)
+        ex_lit = explain_flagged(O, sc, vi, pi, W, H, lit["rgba32f"].reshape(-1, 4)[idx], ref, rays=sub)
     finally:
         sc.close()
-    idx = sub.astype(np.int64)
-    assert (ref["rgba32f"].reshape(-1, 4)[:, 3] > 0).mean() > 0.95
-    _cmp_images(fast["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.01)
-    _cmp_images(lit["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.01)
-    amb = O.ambiguous(ref["margin"])
-    stats = ref["stats"].reshape(-1, 3)
-    assert (fast["hit_counts"].reshape(-1)[idx] != stats[:, 1])[~amb].sum() == 0
-    record_parity("trained", stride=4, **parity_figures(O, gv, fast["rgba32f"].reshape(-1, 4)[idx], ref))
+    record_parity("trained", stride=1, **parity_figures(O, gv, fast["rgba32f"].reshape(-1, 4)[idx], ref), **ex,
+                  literal=ex_lit)
+    assert_explained(ex)
+    assert_explained(ex_lit)

@@ -13,7 +13,9 @@ Tolerances (north star: "pixel-for-pixel within a stated float tolerance", PSNR 
         differently under the GPU's few-ulp exp / rsqrt / rcp and FMA order.  Their fraction is capped per
         configuration near its measured value, and each of them is still bounded: |d rgb| <= the oracle's flip bound
         (oracle.flip_bound: per flagged decision T x alpha moved x the largest radiance channel on the ray, plus
-        minTransmittance x that channel) + 1e-4;
+        minTransmittance x that channel) + 1e-4; and on the full-frame configurations (round 6) each
+        one that differs by more than 1e-4 must equal, to 1e-4, the oracle's re-march of that ray with some of its
+        flagged decisions taken the other way (explain_flagged: single flips, then pairs) -- an exact alternative;
       - every other ray: |d rgb| <= 1e-4 and the accepted-hit count (alpha channel) equal, with no exception
         (frac_tol 0; round 3 allowed 1e-4 of them beyond, up to 5e-3: each of those was an ill-conditioned threshold or
         pair decision, now flagged, DESIGN.md §5);
@@ -522,6 +524,34 @@ def parity_figures(O, gv, got, ref):
                                                 gv.quantize_rgba8(b.astype(np.float32))))}
 
 
+def explain_flagged(O, sc, vi, pi, W, H, got, ref, rays=None, ncams=1, tol=1e-4, max_pairs=4096, **kw):
+    """every flagged ray that the GPU renders more than tol from the oracle must equal, to tol, the
+    oracle's own re-march of that ray with some of its flagged decisions taken the other way (oracle.Scene.explain:
+    each single decision's variants, then pairs of two decisions) -- an exact alternative, not a bound.  got / ref:
+    the compared rays; rays: their indices in the launch (None: 0..n-1).  Returns the figures for record_parity and
+    asserts that none is left unexplained."""
+    g = np.asarray(got, np.float32).reshape(-1, 4)
+    b = np.asarray(ref["rgba32f"], np.float32).reshape(-1, 4)
+    amb = O.ambiguous(ref["margin"])
+    d = np.abs(g[:, :3] - b[:, :3]).max(axis=1)
+    idx = np.nonzero(amb & (d > tol))[0]
+    ids = (np.arange(len(g), dtype=np.uint64) if rays is None else np.asarray(rays, np.uint64).reshape(-1))[idx]
+    ex = sc.explain(vi, pi, W, H, ids, g[idx], tol=tol, max_pairs=max_pairs, ncams=ncams, **kw)
+    ok = ex["dist"] <= tol
+    fig = {"flagged_beyond_1e-4": int(len(idx)), "explained_by_single_flip": int((ok & (ex["kind"] == 1)).sum()),
+           "explained_by_pair": int((ok & (ex["kind"] == 2)).sum()),
+           "flagged_beyond_1e-4_unexplained": int((~ok).sum()),
+           "max_residual_of_explained": float(ex["dist"][ok].max()) if ok.any() else 0.0,
+           "max_decisions_on_a_ray": int(ex["decisions"].max()) if len(idx) else 0,
+           "unexplained_rays": [int(x) for x in ids[~ok][:20]],
+           "unexplained_dist": [float(x) for x in ex["dist"][~ok][:20]]}
+    return fig
+
+
+def assert_explained(fig):
+    assert fig["flagged_beyond_1e-4_unexplained"] == 0, fig
+
+
 def test_bicycle_full_frame_vs_oracle_and_fast_literal(gv, O, bicycle):
     """Config 2 (the bench workload): every one of the 2 073 600 rays of the 1080p frame against the oracle."""
     W, H = 1920, 1080
@@ -541,11 +571,16 @@ def test_bicycle_full_frame_vs_oracle_and_fast_literal(gv, O, bicycle):
     sc = O.Scene(e)
     try:
         ref = sc.render(vi, pi, W, H, margin=True)
+        _cmp_images(fast["rgba32f"], ref, amb_max=0.0152)  # 1.484 % flagged (conditioning-aware flags)
+        _cmp_images(lit["rgba32f"], ref, amb_max=0.0152)
+        ex = explain_flagged(O, sc, vi, pi, W, H, fast["rgba32f"], ref)
+        ex_lit = explain_flagged(O, sc, vi, pi, W, H, lit["rgba32f"], ref)
     finally:
         sc.close()
-    _cmp_images(fast["rgba32f"], ref, amb_max=0.0152)  # 1.484 % flagged (conditioning-aware flags)
-    _cmp_images(lit["rgba32f"], ref, amb_max=0.0152)
-    record_parity("bicycle", **parity_figures(O, gv, fast["rgba32f"], ref), fast_literal_differ=n)
+    record_parity("bicycle", **parity_figures(O, gv, fast["rgba32f"], ref), fast_literal_differ=n, **ex,
+                  literal=ex_lit)
+    assert_explained(ex)
+    assert_explained(ex_lit)
 
 
 def test_unpacked_fast_path_matches(gv, config1):

@@ -241,3 +241,54 @@ def test_cpp_balanced_views_match_python(views, world, seed):
     got = [[int(v) for v in l.split()] for l in lines] + [[] for _ in range(world - len(lines))]
     assert got == dist.balanced_views(costs.tolist(), world)
     assert sorted(v for g in got for v in g) == list(range(views))
+
+
+@pytest.fixture(scope="module")
+def split_fake(tmp_path_factory):
+    """tests/cpp/split_fake.cpp: host/gvrt_split.cpp (the SplitFrame the RCCL build ships, unchanged) over an
+    in-process backend whose ranks are threads (no GPU, no RCCL)."""
+    pkg = os.path.join(ROOT, "3dgvrt_lightfield_amd")
+    exe = str(tmp_path_factory.mktemp("split") / "split_fake")
+    r = subprocess.run(["g++", "-O1", "-std=c++17", "-Wall", "-Werror", "-pthread", "-I", os.path.join(pkg, "host"),
+                        os.path.join(ROOT, "tests", "cpp", "split_fake.cpp"), os.path.join(pkg, "host", "gvrt_split.cpp"),
+                        "-o", exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return exe
+
+
+GVRT_ERR_OOM, GVRT_ERR_HIP, GVRT_ERR_RCCL = -2, -3, -8
+
+
+@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("scenario", ["healthy", "healthy_views", "setup_fail", "stop", "group_fail", "render_fail"])
+def test_split_frame_failure_paths_with_peers(split_fake, scenario, world):
+    """SplitFrame's agree / bounded-wait / abort paths with real peers (SURVEY §5 "Failure detection":
+    statuses, never an abort, replacing VK_CHECK_RESULT, base/VulkanTools.h:42-61), one thread per rank, the wait bound
+    set to 1 s, the whole run under a hard 60 s limit:
+      * healthy (cost bands; views): every frame assembled on rank 0 pixel for pixel, every rank GVRT_OK;
+      * setup_fail: one rank's part-buffer allocation fails -> agree() gives every rank that status (GVRT_ERR_OOM);
+      * stop: one rank stops taking part after its first frame -> every peer returns GVRT_ERR_RCCL within the bound;
+      * group_fail: one rank's send fails inside the frame's group -> group_failed() ends the group and aborts it
+        (GVRT_ERR_RCCL); every peer returns GVRT_ERR_RCCL within the bound;
+      * render_fail: one rank's render fails -> it still enters the exchange, drains it, aborts (GVRT_ERR_HIP); every
+        peer returns GVRT_ERR_RCCL within the bound."""
+    r = subprocess.run([split_fake, scenario, str(world)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    ranks, victim, bound = d["ranks"], d["victim"], d["timeout_s"]
+    peers = [x for x in ranks if x["rank"] != victim]
+    v = ranks[victim]
+    for x in ranks:  # no wait outlives its bound by much: at most two bounded waits per rank here
+        assert x["seconds"] < 2 * bound + 1.0, x
+    if scenario.startswith("healthy"):
+        assert all(x["status"] == 0 and x["frames_ok"] == 4 for x in ranks), ranks
+        assert ranks[0]["frame_ok"]
+    elif scenario == "setup_fail":
+        assert all(x["status"] == GVRT_ERR_OOM and x["frames_ok"] == 0 for x in ranks), ranks
+        assert v["error"] == "part buffer" and all(x["error"] == "set-up failed on another rank" for x in peers)
+    else:
+        want_victim = {"stop": 0, "group_fail": GVRT_ERR_RCCL, "render_fail": GVRT_ERR_HIP}[scenario]
+        assert v["status"] == want_victim and v["frames_ok"] == 1, v
+        assert all(x["status"] == GVRT_ERR_RCCL for x in peers), peers
+        assert all("no progress within" in x["error"] for x in peers), peers
+        assert ranks[0]["frame_ok"]  # the frames completed before the failure were assembled correctly
