@@ -330,6 +330,15 @@ float radianceMax(const Scene& s, uint32_t idx, V3 d, uint32_t sphEvalDegree) {
 // Thresholds of the parity accounting (oracle/oracle.py THR_EPS, PAIR_EPS, BOUND_EPS must equal these:
 // oracle_flag_eps, tests/test_oracle_kat.py)
 constexpr float FLAG_THR_EPS = 1e-4f, FLAG_PAIR_EPS = 2e-6f, FLAG_BOUND_EPS = 1e-5f;
+// Ill-conditioned values (round 6): an accepted crossing whose response is ill-conditioned (a particle far away in
+// kernel units: a tiny Gaussian seen from afar, whose response depends on the ray to ~|gro| ulps) moves the colour by
+// about 2 T a c x its relative change even when no decision is near a threshold.  Per accepted crossing j, v_j = 2 T_j
+// a_j cond_j c (one ulp of its inputs; c the ray's largest radiance channel): a ray whose largest v_j exceeds
+// FLAG_VALUE_EPS (colour units, half the 1e-4 comparison tolerance) is flagged, and its value bound vb =
+// FLAG_VALUE_ULPS x sum_j v_j joins its flip bound.  (Calibrated: an ordinary crossing of the stand-ins has v_j ~ 2e-5,
+// and the GPU's unflagged rays stay within 4.3e-5 of the oracle on 47 M rays; a 1e-4-scale Gaussian 1.8 units away
+// has v_j ~ 3e-4.)
+constexpr float FLAG_VALUE_EPS = 5e-5f, FLAG_VALUE_ULPS = 2.0f;
 // Conditioning-aware margins (unflagged rays beyond 1e-4 were all threshold or pair decisions of
 // ill-conditioned crossings).  A decision is flagged when it lies within its fixed epsilon or within FLAG_COND_ULPS
 // ulps of rounding of its inputs, whichever is larger: a response threshold within FLAG_COND_ULPS x cond (HitEval),
@@ -610,6 +619,8 @@ typedef struct {
 int oracle_version(void) { return 4; }
 
 // the parity accounting's flag thresholds (oracle.py THR_EPS, PAIR_EPS, BOUND_EPS)
+void oracle_value_eps(float* out1) { out1[0] = FLAG_VALUE_EPS; }
+
 void oracle_flag_eps(float* out4) {
     out4[0] = FLAG_THR_EPS;
     out4[1] = FLAG_PAIR_EPS;
@@ -783,6 +794,7 @@ struct RayOut {
     float depth;
     uint32_t stats[3];
     float margin[4];
+    float vbound;  // the ray's value bound (FLAG_VALUE_EPS), with want_margin
 };
 
 }  // extern "C"
@@ -841,6 +853,7 @@ static void marchRay(const OracleScene& os, const oracle_params* P, V3 o, V3 d, 
     // flip bound (margin[3]): summed T x alpha of the flagged decisions, the largest radiance channel
     // involved, and the previous accepted crossing's T before it and alpha (pair swaps)
     float fw = 0.0f, fc = 0.0f, famax = 0.0f, prev_acc_T = 0.0f, prev_acc_a = 0.0f;
+    float vsum = 0.0f, vmax = 0.0f;  // sum and largest of 2 T_j a_j cond_j over accepted crossings (FLAG_VALUE_EPS)
     bool flagged = false;
     uint32_t prev_id_acc = INVALID_PARTICLE_ID;
     uint8_t prev_face = 0, prev_acc_face = 0;
@@ -1045,8 +1058,12 @@ static void marchRay(const OracleScene& os, const oracle_params* P, V3 o, V3 d, 
                         record({Variant{VAR_ACCEPT, 0, 0, h.id, 0.0f, 0}});
                     }
                     if (acc) {
-                        if (ev.galpha < 0.99f)
+                        if (ev.galpha < 0.99f) {
                             t_unc += ev.galpha / (1.0f - ev.galpha) * CU * ev.cond + (CU > 0.0f ? 2.0f * ULP : 0.0f);
+                            const float vj = 2.0f * T_before * ev.galpha * ev.cond;
+                            vsum += vj;
+                            vmax = std::max(vmax, vj);
+                        }
                         const float r2 = std::fabs(st.T / P->min_transmittance - 1.0f);
                         const float te = std::max(FLAG_THR_EPS, t_unc);
                         m_thr = std::min(m_thr, normMargin(r2, FLAG_THR_EPS, te));
@@ -1128,10 +1145,14 @@ static void marchRay(const OracleScene& os, const oracle_params* P, V3 o, V3 d, 
     out.stats[0] = nproc;
     out.stats[1] = nacc;
     out.stats[2] = rounds;
-    out.margin[0] = m_thr;
+    const float vb = FLAG_VALUE_ULPS * vsum * fc;
+    const bool vflag = want_margin && vmax * fc > FLAG_VALUE_EPS;
+    out.vbound = vb;
+    out.margin[0] = vflag ? 0.0f : m_thr;  // an ill-conditioned value: flagged like a decision on its threshold
     out.margin[1] = m_t;
     out.margin[2] = m_b;
-    out.margin[3] = flagged ? (fw + P->min_transmittance / std::max(1.0f - famax, 0.01f)) * fc : 0.0f;
+    out.margin[3] = (flagged ? (fw + P->min_transmittance / std::max(1.0f - famax, 0.01f)) * fc : 0.0f) +
+                    (flagged || vflag ? vb : 0.0f);
 }
 
 // ray r of a launch: its origin and direction (with the parity accounting's perturbation, if any)
@@ -1255,8 +1276,9 @@ int oracle_scene_render(void* h, const oracle_params* P, const float* viewInvers
 // decisions taken the other way.  For each ray rays[k] the march records every flagged decision's variants
 // (Variant); the alternatives are the base march, each single variant, then each pair of variants of two different
 // decisions (at most max_pairs pairs), tried in that order until one lies within tol of target[3k .. 3k+2] (max
-// |d rgb|).  out[4k ..]: {the distance of the nearest alternative tried, its kind (0 base, 1 single, 2 pair), the
-// number of variants, the number of decisions}.  alt_rgba (optional, 4 floats per ray): that alternative's colour.
+// |d rgb|, less the alternative's own value bound, FLAG_VALUE_EPS).  out[5k ..]: {the distance of the best
+// alternative, its kind (0 base, 1 single, 2 pair), the number of variants, the number of decisions, its value
+// bound}.  alt_rgba (optional, 4 floats per ray): that alternative's colour.
 int oracle_scene_explain(void* h, const oracle_params* P, const float* viewInverse, const float* projInverse,
                          uint32_t W, uint32_t H, uint32_t ncams, const uint64_t* rays, uint64_t n, const float* target,
                          float tol, uint32_t max_pairs, float* out, float* alt_rgba, int nthreads) {
@@ -1275,12 +1297,14 @@ int oracle_scene_explain(void* h, const oracle_params* P, const float* viewInver
         RayOut base;
         marchRay(*os, P, o, d, true, nullptr, &vars, base);
         const float* tg = target + 3 * k;
+        // an alternative explains the target when it lies within tol plus the alternative's own value bound (the
+        // colour its ill-conditioned responses may move, FLAG_VALUE_EPS); the excess over that is what is minimised
         auto dist = [&](const RayOut& ro) {
             float m = 0.0f;
             for (int c = 0; c < 3; ++c) m = std::max(m, std::fabs(ro.rgba[c] - tg[c]));
             return m;
         };
-        float best = dist(base);
+        float best = dist(base) - base.vbound;
         int kind = 0;
         RayOut best_out = base;
         uint32_t ngroups = vars.empty() ? 0u : vars.back().group + 1u;
@@ -1289,8 +1313,8 @@ int oracle_scene_explain(void* h, const oracle_params* P, const float* viewInver
             F.v = v;
             F.n = nv;
             RayOut ro;
-            marchRay(*os, P, o, d, false, &F, nullptr, ro);
-            const float dd = dist(ro);
+            marchRay(*os, P, o, d, true, &F, nullptr, ro);
+            const float dd = dist(ro) - ro.vbound;
             if (dd < best) {
                 best = dd;
                 kind = knd;
@@ -1306,10 +1330,11 @@ int oracle_scene_explain(void* h, const oracle_params* P, const float* viewInver
                 consider(two, 2, 2);
                 ++pairs;
             }
-        out[4 * k] = best;
-        out[4 * k + 1] = (float)kind;
-        out[4 * k + 2] = (float)vars.size();
-        out[4 * k + 3] = (float)ngroups;
+        out[5 * k] = dist(best_out);
+        out[5 * k + 1] = (float)kind;
+        out[5 * k + 2] = (float)vars.size();
+        out[5 * k + 3] = (float)ngroups;
+        out[5 * k + 4] = best_out.vbound;
         if (alt_rgba)
             for (int c = 0; c < 4; ++c) alt_rgba[4 * k + c] = best_out.rgba[c];
     }

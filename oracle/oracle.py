@@ -208,9 +208,10 @@ class Scene:
     def explain(self, view_inv, proj_inv, width, height, rays, target_rgb, tol=1e-4, max_pairs=4096, ncams=1,
                 threads=0, **kw):
         """Each ray re-marched with its flagged decisions taken the other way (oracle_scene_explain): the base march,
-        each single variant, then pairs of variants of two different decisions, until one is within tol (max |d rgb|)
-        of target_rgb (n x 3, e.g. the GPU's values).  Returns dict(dist, kind (0 base, 1 single flip, 2 pair),
-        variants, decisions, alt_rgba)."""
+        each single variant, then pairs of variants of two different decisions, until one is within tol plus its own
+        value bound (max |d rgb|; FLAG_VALUE_EPS in gvrt_oracle.cpp) of target_rgb (n x 3, e.g. the GPU's values).
+        Returns dict(dist, kind (0 base, 1 single flip, 2 pair), variants, decisions, vbound, alt_rgba): a ray is
+        explained when dist <= tol + vbound."""
         p = default_params(proxy_mode=self.proxy_mode, **self.kw, **kw)
         vi = np.ascontiguousarray(view_inv, np.float32).reshape(-1)
         pi = np.ascontiguousarray(proj_inv, np.float32).reshape(16)
@@ -218,14 +219,14 @@ class Scene:
         tg = np.ascontiguousarray(np.asarray(target_rgb, np.float32).reshape(-1, 4)[:, :3]
                                   if np.asarray(target_rgb).reshape(len(r), -1).shape[1] == 4
                                   else np.asarray(target_rgb, np.float32).reshape(-1, 3))
-        out = np.zeros((len(r), 4), np.float32)
+        out = np.zeros((len(r), 5), np.float32)
         alt = np.zeros((len(r), 4), np.float32)
         if len(r):
             rc = lib().oracle_scene_explain(self.h, C.byref(p), _p(vi), _p(pi), width, height, ncams, _p(r), len(r),
                                             _p(tg), float(tol), int(max_pairs), _p(out), _p(alt), int(threads))
             assert rc == 0, rc
         return {"dist": out[:, 0], "kind": out[:, 1].astype(np.int32), "variants": out[:, 2].astype(np.int32),
-                "decisions": out[:, 3].astype(np.int32), "alt_rgba": alt}
+                "decisions": out[:, 3].astype(np.int32), "vbound": out[:, 4], "alt_rgba": alt}
 
     def trace(self, view_inv, proj_inv, width, height, ray, ncams=1, maxn=4096, **kw):
         """Processed crossings of one ray (debugging): array of (id, t, gres, galpha, T after, accepted, round)."""

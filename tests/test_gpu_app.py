@@ -74,7 +74,13 @@ def test_bench_on_a_ply(gv, tmp_path):
     assert roof["bound"] in ("issue", "hbm") and roof["frac"] <= 1.0, roof
     # the bound names the busier resource: VALU issue unless the HBM fraction is larger
     assert (roof["bound"] == "hbm") == (roof["hbm"]["frac"] > roof.get("valu_issue_frac", roof["frac"])), roof
-    assert 0.0 < roof["hbm"]["frac"] < 1.0 and roof["logical"]["bound"] == "hbm"
+    assert 0.0 < roof["hbm"]["frac"] < 1.0
+    # round 6: the reference-gather figure carries no bound and no fraction; every fraction the line
+    # states is <= 1 and the largest names the binding unit
+    assert "bound" not in roof["reference_gather"] and "frac" not in roof["reference_gather"]
+    fr = roof["binding"]["fractions"]
+    assert all(0.0 <= v <= 1.0 for v in fr.values()) and roof["binding"]["largest"] == max(fr, key=fr.get), roof
+    assert 0.0 < roof["cache"]["l2_hit_rate"] <= 1.0 and roof["latency"]["node_visits_per_wave"] > 0
 
 
 def test_cpp_app_flows_match_python(gv, tmp_path):

@@ -327,3 +327,50 @@ def test_conditioning_flags_catch_the_r03_outlier_class(gv, O, mipnerf_small):
     moved = a["stats"][:, 1] != b["stats"][:, 1]
     assert (moved & ~amb0).sum() >= 3 and ((d > 1e-4) & ~amb0).sum() >= 3
     assert not (moved & ~amb).any() and not ((d > 1e-4) & ~amb).any()
+
+
+def test_explain_reproduces_other_float_evaluations(gv, O):
+    """The alternatives of oracle.Scene.explain on the oracle itself: the same frame evaluated with
+    every ray's inputs moved by 1 or 2 ulps (perturb_ulps: another float evaluation, as the GPU's) differs on a few
+    rays by more than 1e-4; each of them is flagged, and each equals the unperturbed march of that ray with some of
+    its flagged decisions taken the other way (a single flip here), within 1e-4 plus its value bound."""
+    s = gv.scene.mipnerf_standin(200_000, seed=9)
+    e = O.enclose(s)
+    sc = O.Scene(e)
+    W, H = 640, 360
+    vi, pi = gv.scene.mipnerf_camera(W, H)
+    try:
+        base = sc.render(vi, pi, W, H, margin=True)
+        b = base["rgba32f"].reshape(-1, 4)
+        amb = O.ambiguous(base["margin"])
+        for pu in (1, 2):
+            alt = sc.render(vi, pi, W, H, margin=True, perturb_ulps=pu)["rgba32f"].reshape(-1, 4)
+            d = np.abs(alt[:, :3] - b[:, :3]).max(axis=1)
+            idx = np.nonzero(d > 1e-4)[0]
+            assert len(idx) >= 10 and amb[idx].all(), (pu, len(idx), int(amb[idx].sum()))
+            ex = sc.explain(vi, pi, W, H, idx.astype(np.uint64), alt[idx])
+            assert (ex["dist"] <= 1e-4 + ex["vbound"]).all(), (pu, ex)
+            assert (ex["kind"] >= 1).mean() > 0.8  # mostly exact decision flips, not value bounds
+    finally:
+        sc.close()
+
+
+def test_value_flag_on_ill_conditioned_response(gv, O):
+    """FLAG_VALUE_EPS (round 6): a tiny Gaussian (scale 1e-4) 1.8 units from the camera has a response that depends
+    on the ray to ~2e4 ulps of its kernel-frame origin, so its colour moves by ~1e-4 under another float evaluation
+    with no decision near a threshold; the ray is flagged and carries a value bound.  The same Gaussian at scale 0.05
+    is not flagged."""
+    rd = (math.log(0.2) / -0.0555555555556) ** 0.25  # kernel-frame line distance of a response 0.2
+
+    def one(scale):
+        e = O.enclose(one_gaussian(scale=scale, opacity=2.0, fdc=(0.5, 0.2, 0.1), frest=np.full(45, 0.01)))
+        assert e["m"] == 1
+        x = rd * scale  # the optical axis passes at x from the centre
+        vi, pi = gv.camera.pinhole((x, 0.0, 1.8), (x, 0.0, 0.0), (0.0, 1.0, 0.0), 60.0, 1.0)
+        r = O.render(e, vi, pi, 2, 2, proxy_mode=1)  # pixel (1, 1) of a 2x2 image: the optical axis
+        return r["rgba32f"][0, 1, 1], r["margin"][0, 1, 1]
+    (tiny, mt), (big, mb) = one(1e-4), one(0.05)
+    assert tiny[3] == 2 and big[3] == 2  # both crossings composited
+    np.testing.assert_allclose(tiny[:3], big[:3], rtol=2e-3)  # the same colour, whatever the scale
+    assert O.ambiguous(mt[None]).all() and O.flip_bound(mt[None])[0] > 5e-5
+    assert not O.ambiguous(mb[None]).any() and O.flip_bound(mb[None])[0] == 0.0
