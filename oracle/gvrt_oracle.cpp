@@ -883,6 +883,7 @@ static void marchRay(const OracleScene& os, const oracle_params* P, V3 o, V3 d, 
     bool round_start = false;
     uint32_t prev_id = INVALID_PARTICLE_ID;
     std::vector<uint32_t> last_ids;  // ids processed with t == last (tie detection, margin)
+    std::vector<uint8_t> last_faces;  // and which crossing of each
     std::vector<uint32_t> stack;
     stack.reserve(128);
     while (last <= tmaxb && alive()) {
@@ -903,8 +904,14 @@ static void marchRay(const OracleScene& os, const oracle_params* P, V3 o, V3 d, 
                     const HitEval he = evalResponse(s, pid, o, d);
                     if (he.gres > P->hit_min_gaussian_response && he.galpha > P->alpha_min) {
                         flag(T_round, he.galpha, pid);
-                        // the other evaluation finds it just past `last`
-                        record({Variant{VAR_SET_T, face, 0, pid, std::nextafter(last, INFINITY), 0}});
+                        // the other evaluation finds it just past `last`, or took it in the previous round in place
+                        // of the crossing that set `last` (tied: arrival order), which is then the one dropped
+                        if (!last_ids.empty())
+                            record({Variant{VAR_SET_T, face, 0, pid, std::nextafter(last, INFINITY), 0},
+                                    Variant{VAR_SET_T, face, 0, pid, std::nextafter(last, -INFINITY), 0},
+                                    Variant{VAR_DROP, last_faces.back(), 0, last_ids.back(), 0.0f, 0}});
+                        else
+                            record({Variant{VAR_SET_T, face, 0, pid, std::nextafter(last, INFINITY), 0}});
                     }
                 }
                 return;
@@ -1024,8 +1031,11 @@ static void marchRay(const OracleScene& os, const oracle_params* P, V3 o, V3 d, 
             if (gg < ge) {
                 flag(T_round, evalResponse(s, k15.id, o, d).galpha, k15.id);
                 flag(T_round, evalResponse(s, h_out.id, o, d).galpha, h_out.id);
-                // the other evaluation takes the crossing left out into this round instead
-                record({Variant{VAR_SET_T, h_out.face, 0, h_out.id, std::nextafter(k15.t, -INFINITY), 0}});
+                // the other evaluation takes the crossing left out into this round instead; tied, the one that
+                // arrives second is found again at `last` in the next round and dropped (exclusive tmin, Q13)
+                record({Variant{VAR_SET_T, h_out.face, 0, h_out.id, std::nextafter(k15.t, -INFINITY), 0},
+                        Variant{VAR_DROP, k15.face, 0, k15.id, 0.0f, 0},
+                        Variant{VAR_DROP, h_out.face, 0, h_out.id, 0.0f, 0}});
             }
         }
         round_start = true;
@@ -1113,8 +1123,8 @@ static void marchRay(const OracleScene& os, const oracle_params* P, V3 o, V3 d, 
                         prev_id_acc = h.id;
                         prev_acc_face = h.face;
                     }
-                    if (h.t > last) last_ids.clear();
-                    if (h.t >= last) last_ids.push_back(h.id);
+                    if (h.t > last) last_ids.clear(), last_faces.clear();
+                    if (h.t >= last) last_ids.push_back(h.id), last_faces.push_back(h.face);
                     // the crossing that ends the ray against its successor: a tie decides which of
                     // the two is composited
                     // (only an accepted successor changes the image by coming first)
@@ -1129,7 +1139,11 @@ static void marchRay(const OracleScene& os, const oracle_params* P, V3 o, V3 d, 
                             if (gg < ge) {
                                 flag(T_before, ev.galpha, h.id);
                                 flag(T_before, evalResponse(s, nx.id, o, d).galpha, nx.id);
-                                record({Variant{VAR_SET_T, nx.face, 0, nx.id, std::nextafter(h.t, -INFINITY), 0}});
+                                // the successor comes first; or, tied bitwise with it, the successor takes the last
+                                // slot of a full buffer of the other evaluation (FAST: 32 accepted), the round ends
+                                // there and this crossing is lost to the exclusive tmin (Q13)
+                                record({Variant{VAR_SET_T, nx.face, 0, nx.id, std::nextafter(h.t, -INFINITY), 0},
+                                        Variant{VAR_DROP, h.face, 0, h.id, 0.0f, 0}});
                             }
                         }
                     }

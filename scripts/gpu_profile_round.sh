@@ -37,7 +37,7 @@ fi
 [ "$PART" = "1" ] && exit 0
 for cfg in garden truck lightfield dense; do
   timeout -k 10 300 python bench.py --config $cfg --steps 20 --warmup 3 --no-cpu-baseline > $out/config_$cfg.json 2> $out/config_$cfg.err || { echo "$cfg failed"; tail -5 $out/config_$cfg.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$out/config_$cfg.json')); r=d['roofline']; print('$cfg', d['value'], d['ms_per_step'], d['kernel_ms'], r['bound'], r['frac'], r.get('logical', {}).get('frac'), r.get('hbm', {}).get('frac'))"
+  python3 -c "import json; d=json.load(open('$out/config_$cfg.json')); r=d['roofline']; print('$cfg', d['value'], d['ms_per_step'], d['kernel_ms'], r['bound'], r['frac'], r.get('cache', {}).get('l2_frac'), r.get('latency', {}).get('frac'), r.get('hbm', {}).get('frac'))"
 done
 for cfg in bicycle dense; do
   timeout -k 10 200 python3 scripts/orbit_costs_dump.py $out/orbit_costs_$cfg.npz $cfg 0.1 0.5 2 > $out/orbit_costs_$cfg.log 2>&1 || { echo "orbit costs $cfg failed"; tail -5 $out/orbit_costs_$cfg.log; exit 1; }

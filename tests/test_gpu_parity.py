@@ -550,7 +550,9 @@ def explain_flagged(O, sc, vi, pi, W, H, got, ref, rays=None, ncams=1, tol=1e-4,
            "max_residual_of_explained": float(ex["dist"][ok].max()) if ok.any() else 0.0,
            "max_decisions_on_a_ray": int(ex["decisions"].max()) if len(idx) else 0,
            "unexplained_rays": [int(x) for x in ids[~ok][:20]],
-           "unexplained_dist": [float(x) for x in ex["dist"][~ok][:20]]}
+           "unexplained_dist": [float(x) for x in ex["dist"][~ok][:20]],
+           "unexplained_gpu_rgba": [[float(v) for v in g[i]] for i in idx[~ok][:20]],
+           "unexplained_vbound": [float(x) for x in ex["vbound"][~ok][:20]]}
     return fig
 
 
