@@ -5,6 +5,7 @@ exists for this path, so the oracle is pinned here by closed-form 
 independent numpy restatement of the enclosing filter / SH evaluation, by the agreement of its
 literal 20-triangle mode with its analytic mode, and by committed golden fixtures.
 """
+import json
 import math
 import os
 
@@ -374,3 +375,29 @@ def test_value_flag_on_ill_conditioned_response(gv, O):
     np.testing.assert_allclose(tiny[:3], big[:3], rtol=2e-3)  # the same colour, whatever the scale
     assert O.ambiguous(mt[None]).all() and O.flip_bound(mt[None])[0] > 5e-5
     assert not O.ambiguous(mb[None]).any() and O.flip_bound(mb[None])[0] == 0.0
+
+
+@pytest.mark.timeout(300)
+def test_explain_reproduces_gpu_termination_ties(gv, O):
+    """Three light-field rays whose GPU (FAST, 32 slots) colour no alternative explained in round 6 run d, with the
+    GPU's values kept as a fixture (tests/golden/lightfield_fast_boundary_r06.json): the terminating crossing ties
+    with its successor, and on the GPU the successor fills the last slot and the terminating crossing is lost to the
+    exclusive tmin at the round boundary.  The oracle records that drop as an alternative of the flagged tie, and the
+    re-march reproduces each GPU value to 2e-6 with its accepted-hit count."""
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "lightfield_fast_boundary_r06.json")))
+    gen, W, H, ncams = gv.scene.CONFIGS[fx["config"]]
+    r = fx["rig"]
+    vi, pi = gv.camera.lightfield_grid_rig(gv.camera.orbit_eye(*r["eye"]), (0.0, 0.0, 0.0), nx=r["nx"], ny=r["ny"],
+                                           spacing=r["spacing"], aspect=gv.camera.aspect_ratio(W, H))
+    sc = O.Scene(O.enclose(gv.scene.make(**gen)))
+    try:
+        rays = np.array(fx["rays"], np.uint64)
+        gpu = np.array(fx["gpu_rgba"], np.float32)
+        ref = sc.render(vi, pi, W, H, ncams=ncams, subset=rays, margin=True)
+        assert O.ambiguous(ref["margin"]).all()
+        assert (np.abs(ref["rgba32f"][:, :3] - gpu[:, :3]).max(axis=1) > 1e-4).all()  # they do differ
+        ex = sc.explain(vi, pi, W, H, rays, gpu, ncams=ncams)
+        assert (ex["kind"] == 1).all() and (ex["dist"] <= 2e-6).all(), ex
+        np.testing.assert_array_equal(ex["alt_rgba"][:, 3], gpu[:, 3])
+    finally:
+        sc.close()
