@@ -3,7 +3,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r06
 export TMPDIR=/tmp
-timeout -k 10 1080 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread > gpurun_out/r06/tests_e.log 2>&1
+timeout -k 10 1080 python -u -m pytest tests -m gpu -v --timeout 900 --timeout-method thread > gpurun_out/r06/tests_e.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/r06/tests_e.log
 tail -4 gpurun_out/r06/tests_e.log
