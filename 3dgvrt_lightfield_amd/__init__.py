@@ -11,8 +11,8 @@ except Exception:  # pragma: no cover - torch is optional for the C-ABI path
 
 from . import camera, scene  # noqa: E402
 from ._lib import GvrtError, LIB_PATH, MODE_FAST, MODE_LITERAL, lib  # noqa: E402
-from .renderer import (PLYLoader, Renderer, SplatSet, device_count, device_properties, psnr_rgb, quantize_rgba8,  # noqa: E402
+from .renderer import (QUALITY_BUILD, PLYLoader, Renderer, SplatSet, device_count, device_properties, psnr_rgb, quantize_rgba8,  # noqa: E402
                        save_ply, tiles_for_rank)
 
-__all__ = ["camera", "scene", "GvrtError", "LIB_PATH", "MODE_FAST", "MODE_LITERAL", "lib", "PLYLoader",
+__all__ = ["camera", "scene", "GvrtError", "LIB_PATH", "MODE_FAST", "MODE_LITERAL", "lib", "QUALITY_BUILD", "PLYLoader",
            "Renderer", "SplatSet", "device_count", "device_properties", "psnr_rgb", "quantize_rgba8", "save_ply", "tiles_for_rank"]

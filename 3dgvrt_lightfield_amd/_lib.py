@@ -80,7 +80,7 @@ class Image(C.Structure):
 
 class AccelParams(C.Structure):
     _fields_ = [("split_cells", C.c_uint32), ("builder", C.c_uint32), ("collapse", C.c_uint32),
-                ("depth_budget", C.c_uint32), ("reserved", C.c_uint32 * 4)]
+                ("depth_budget", C.c_uint32), ("split_min_span", C.c_uint32), ("reserved", C.c_uint32 * 3)]
 
 
 class Stats(C.Structure):

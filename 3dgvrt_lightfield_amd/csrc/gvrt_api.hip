@@ -261,6 +261,8 @@ gvrt_status gvrt_build_accel_ex(gvrt_handle c, const gvrt_accel_params* p) {
         return gvrt_fail(c, GVRT_ERR_INVALID_ARG,
                          "builder must be 0 (LBVH), 1 (PLOC), 2 (binned SAH, device) or 3 (binned SAH, host)");
     if (p->collapse > 1) return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "collapse must be 0 (greedy) or 1 (SAH-optimal DP)");
+    if (p->split_min_span > 1023)
+        return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "split_min_span must be at most 1023");
     if (p->depth_budget > gvrt::SAH_DEPTH_MAX)
         return gvrt_fail(c, GVRT_ERR_INVALID_ARG, "depth_budget must be 0 (default) or at most 43");
     GVRT_HIP(c, hipSetDevice(c->device));
@@ -619,15 +621,16 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
     std::memset(&a, 0, sizeof(a));
     a.recs = c->d_recs;
     // split: the k-buffer holds proxy (compaction) ids, shared by the proxy's pieces
-    a.crecs = c->split_cells ? c->d_recs_c : c->d_recs;
-    a.sh = c->split_cells ? c->d_sh48 : c->d_sh;
+    a.crecs = c->d_recs;
+    a.sh = c->d_sh;
     a.aux = reinterpret_cast<const uint4*>(c->d_leaf_aux);
     for (int k = 0; k < 3; ++k) a.grid_min[k] = c->grid_min[k];
     a.grid_inv = c->grid_inv;
     a.nodes = c->d_nodes4;
     a.nodes8 = c->opt[GVRT_OPT_OCTANT_NODES] ? c->d_nodes4x8 : nullptr;
     a.nodes8_stride = c->n_nodes4;
-    a.nrecs = (uint32_t)c->m;
+    // k-buffer payloads are leaf indices (split pieces included): the packed buffer's 24-bit ids bound the leaves
+    a.nrecs = (uint32_t)std::max<uint64_t>(c->m, c->n_leaves);
     // the render kernel addresses leaf records (64 B) and 4-wide nodes (128 B) by 32-bit byte offsets
     if (c->n_leaves >= (1ull << 26) || c->n_nodes4 >= (1ull << 25))
         return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "more than 2^26 BVH leaves or 2^25 nodes (32-bit record offsets)");
@@ -698,7 +701,7 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         float omax = 0.0f;
         for (uint32_t i = 0; i < ncams; ++i)
             for (int k = 12; k < 15; ++k) omax = std::max(omax, std::fabs(view_inverse[16ull * i + k]));
-        a.box_exact = c->opt[GVRT_OPT_BOX_SLACK] == 0 && !c->split_cells && c->box_pad_abs > 0.0f &&
+        a.box_exact = c->opt[GVRT_OPT_BOX_SLACK] == 0 && c->box_pad_abs > 0.0f &&
                       std::ldexp(omax, -20) <= c->box_pad_abs;  // also false for a NaN origin
     }
     a.kfast = p->kbuffer_depth ? p->kbuffer_depth : (uint32_t)K_FAST_DEFAULT;
@@ -711,7 +714,7 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
     // thresholds change; LITERAL launches keep every crossing and so the proxy boxes.  A negative alphaMin keeps the
     // proxy boxes too: a particle of density rho <= alphaMin < 0 is then accepted in a shell (min(0.99, gres rho) >
     // alphaMin for small gres), not inside a ball, so neither its acceptance ball nor its drop would be exact
-    if (p->mode == GVRT_MODE_FAST && c->opt[GVRT_OPT_ACCEPT_BOXES] && !c->split_cells && p->alpha_min >= 0.0f &&
+    if (p->mode == GVRT_MODE_FAST && c->opt[GVRT_OPT_ACCEPT_BOXES] && p->alpha_min >= 0.0f &&
         (p->hit_min_gaussian_response > 0.0f || p->alpha_min > 0.0f) && a.nrecs < 0xFFFFFFu &&
         c->opt[GVRT_OPT_PACKED_KBUFFER]) {
         if (!c->accept_ok || c->accept_key[0] != p->hit_min_gaussian_response || c->accept_key[1] != p->alpha_min)
@@ -731,7 +734,7 @@ static gvrt_status render_impl(gvrt_handle c, const gvrt_render_params* p, const
         const bool adaptive = (c->enc.opts & 1u) != 0;
         const bool okbase = c->opt[GVRT_OPT_RECORD_ORIGINS] && p->mode == GVRT_MODE_FAST &&
                             a.kfast == (uint32_t)K_FAST_DEFAULT && !adaptive && a.nrecs < 0xFFFFFFu &&
-                            c->opt[GVRT_OPT_PACKED_KBUFFER] && c->n_leaves && !c->split_cells;
+                            c->opt[GVRT_OPT_PACKED_KBUFFER] && c->n_leaves;
         a.okrec = okbase && one_origin;
         const uint64_t cams_bytes = (uint64_t)ncams * c->n_leaves * sizeof(RenderRec);
         // (the copies are an optional speed-up: one that does not fit leaves the launch on d_recs, okrec = 0, until

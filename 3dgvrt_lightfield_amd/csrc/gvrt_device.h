@@ -67,7 +67,8 @@ struct alignas(16) Bvh4Node {  // (name kept from the 4-wide layout; BVH_W child
     float box[BVH_W][6];   // [child][lx, hx, ly, hy, lz, hz]
     int32_t child[BVH_W];  // >= 0: node index; < 0: leaf ~record index
     uint32_t nchild;
-    uint32_t pad[3];       // [0] split axis of the children's order (0 x, 1 y, 2 z), [1] internal-child mask
+    uint32_t pad[3];       // [0] split axis of the children's order (0 x, 1 y, 2 z), [1] internal-child mask (bits
+                           // 0-3) | split-piece leaf mask << 4 (leaves with a cell test), [2] acceptance widening D
 };
 static_assert(sizeof(Bvh4Node) == 28 * BVH_W + 16, "node layout: 128 B (4-wide) / 240 B (8-wide)");
 

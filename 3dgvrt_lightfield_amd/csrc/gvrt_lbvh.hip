@@ -140,8 +140,8 @@ __global__ __launch_bounds__(256) void k_morton(uint64_t m, const float* __restr
 }
 
 // Leaf order: leaf j takes sorted item perm[j] (a proxy, or a split piece whose proxy is psrc[.]).
-// Records are copied per leaf; the SH only without split (with split the k-buffer payload is the
-// proxy id and the SH / composite records stay in compaction order).
+// Records and SH are copied per leaf, pieces included: the k-buffer payload is the leaf index, so the
+// composite, the origin record copies and the acceptance boxes read per-leaf arrays with or without split.
 __global__ __launch_bounds__(256) void k_permute(uint64_t m, const uint32_t* __restrict__ perm, const RenderRec* __restrict__ rin,
                                                  const float* __restrict__ shin, const float* __restrict__ bin,
                                                  const uint4* __restrict__ paux, RenderRec* __restrict__ rout,
@@ -177,17 +177,33 @@ __device__ inline int grid_cell(const Grid& g, int a, float x) {
     return i < 0 ? 0 : (i >= (int)g.n[a] ? (int)g.n[a] - 1 : i);
 }
 
+// A proxy is split when its box overlaps at least min_span cells along one axis (min_span <= 2: every proxy that
+// overlaps more than one cell, the reference's rule); a smaller one stays one piece that admits every crossing.
+__device__ inline bool piece_single(const int lo[3], const int hi[3], uint32_t min_span) {
+    int span = 0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) span = max(span, hi[a] - lo[a] + 1);
+    return span < (int)(min_span > 2u ? min_span : 2u);
+}
+
 __global__ __launch_bounds__(256) void k_piece_count(uint64_t m, const float* __restrict__ boxes, Grid g,
-                                                     uint64_t* __restrict__ cnt) {
+                                                     uint32_t min_span, uint64_t* __restrict__ cnt) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > m) return;
     if (i == m) {
         cnt[i] = 0;
         return;
     }
-    uint64_t c = 1;
+    int lo[3], hi[3];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) c *= (uint64_t)(grid_cell(g, a, boxes[6 * i + 3 + a]) - grid_cell(g, a, boxes[6 * i + a]) + 1);
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = grid_cell(g, a, boxes[6 * i + a]);
+        hi[a] = grid_cell(g, a, boxes[6 * i + 3 + a]);
+    }
+    uint64_t c = 1;
+    if (!piece_single(lo, hi, min_span))
+#pragma unroll
+        for (int a = 0; a < 3; ++a) c *= (uint64_t)(hi[a] - lo[a] + 1);
     cnt[i] = c;
 }
 
@@ -201,8 +217,8 @@ __device__ inline uint32_t pack_cell(int x, int y, int z) { return (uint32_t)x |
 // crosses a clipped triangle only inside its cell.  A proxy inside one cell keeps its box and cell
 // "any" (0xFFFFFFFF: no point test).
 __global__ __launch_bounds__(256) void k_piece_emit(uint64_t m, const float* __restrict__ boxes, Grid g,
-                                                    const uint64_t* __restrict__ off, float* __restrict__ pbox,
-                                                    uint4* __restrict__ paux) {
+                                                    uint32_t min_span, float pad_abs, const uint64_t* __restrict__ off,
+                                                    float* __restrict__ pbox, uint4* __restrict__ paux) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     int lo[3], hi[3];
@@ -212,7 +228,16 @@ __global__ __launch_bounds__(256) void k_piece_emit(uint64_t m, const float* __r
         hi[a] = grid_cell(g, a, boxes[6 * i + 3 + a]);
     }
     uint64_t p = off[i];
-    const bool single = lo[0] == hi[0] && lo[1] == hi[1] && lo[2] == hi[2];
+    const bool single = piece_single(lo, hi, min_span);
+    if (single) {  // one piece: the proxy's own box, every crossing admitted
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            pbox[6 * p + a] = boxes[6 * i + a];
+            pbox[6 * p + 3 + a] = boxes[6 * i + 3 + a];
+        }
+        paux[p] = make_uint4((uint32_t)i, 0xFFFFFFFFu, 0u, 0u);
+        return;
+    }
     const uint32_t plo = pack_cell(lo[0], lo[1], lo[2]), phi = pack_cell(hi[0], hi[1], hi[2]);
     for (int iz = lo[2]; iz <= hi[2]; ++iz)
         for (int iy = lo[1]; iy <= hi[1]; ++iy)
@@ -221,18 +246,32 @@ __global__ __launch_bounds__(256) void k_piece_emit(uint64_t m, const float* __r
 #pragma unroll
                 for (int a = 0; a < 3; ++a) {
                     const float bl = boxes[6 * i + a], bh = boxes[6 * i + 3 + a];
-                    if (single) {
-                        pbox[6 * p + a] = bl;
-                        pbox[6 * p + 3 + a] = bh;
-                        continue;
-                    }
                     const float cl = g.mn[a] + (float)ci[a] * g.size, ch = g.mn[a] + (float)(ci[a] + 1) * g.size;
-                    const float pad = 1e-5f * g.size + 1e-6f * fmaxf(fabsf(cl), fabsf(ch));
+                    // (+ the proxy boxes' absolute padding, so a cell face covers the render kernel's plane
+                    // rounding as a proxy face does: RenderArgs::box_exact)
+                    const float pad = 1e-5f * g.size + 1e-6f * fmaxf(fabsf(cl), fabsf(ch)) + pad_abs;
                     pbox[6 * p + a] = fmaxf(bl, cl - pad);
                     pbox[6 * p + 3 + a] = fminf(bh, ch + pad);
                 }
-                paux[p] = make_uint4((uint32_t)i, single ? 0xFFFFFFFFu : pack_cell(ix, iy, iz), plo, phi);
+                paux[p] = make_uint4((uint32_t)i, pack_cell(ix, iy, iz), plo, phi);
             }
+}
+
+// Split builds: bit 4 + k of pad[1] marks leaf child k as a piece with a cell (its crossings need the cell test,
+// gvrt_render.hip GVRT_LEAF); the render kernel loads a leaf's aux record only for those, so the proxies a split
+// leaves whole cost what they cost without split
+__global__ __launch_bounds__(256) void k_mark_pieces(uint64_t n, Bvh4Node* __restrict__ nodes,
+                                                     const uint4* __restrict__ aux) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int k = 0; k < BVH_W; ++k) {
+        const int32_t ch = nodes[i].child[k];
+        if (nodes[i].box[k][0] > 1e37f || ch >= 0) continue;  // empty slot or inner child
+        if (aux[~ch].y != 0xFFFFFFFFu) bits |= 16u << k;
+    }
+    nodes[i].pad[1] = (nodes[i].pad[1] & 0xFu) | bits;
 }
 
 // Range-union sparse table over the leaf boxes (leaf order): level k holds, for every i, the union of
@@ -869,7 +908,7 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
         TRY(gvrt_dalloc(c, (void**)&pcnt, 8ull * (mp + 1)));
         TRY(gvrt_dalloc(c, (void**)&poff, 8ull * (mp + 1)));
         hipLaunchKernelGGL(k_piece_count, dim3((unsigned)((mp + 1 + 255) / 256)), dim3(256), 0, c->stream, (uint64_t)mp,
-                           c->d_boxes_c, g, pcnt);
+                           c->d_boxes_c, g, ap.split_min_span, pcnt);
         size_t pt = 0;
         TRYH(hipcub::DeviceScan::ExclusiveSum(nullptr, pt, pcnt, poff, (int)(mp + 1), c->stream), "scan size");
         TRY(gvrt_dalloc(c, &ptmp, pt ? pt : 16));
@@ -881,19 +920,22 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
             cleanup();
             return gvrt_fail(c, GVRT_ERR_UNSUPPORTED, "split produced an unsupported number of pieces");
         }
-        m = np;
-        TRY(gvrt_dalloc(c, (void**)&pbox, 24ull * m));
-        TRY(gvrt_dalloc(c, (void**)&paux, 16ull * m));
-        hipLaunchKernelGGL(k_piece_emit, dim3(pb), dim3(256), 0, c->stream, (uint64_t)mp, c->d_boxes_c, g, poff, pbox,
-                           paux);
-        TRYH(hipGetLastError(), "k_piece_emit");
-        boxes_in = pbox;
-        c->split_cells = ap.split_cells;
-        for (int a = 0; a < 3; ++a) {
-            c->grid_min[a] = g.mn[a];
-            c->grid_n[a] = g.n[a];
+        // no proxy split (every one inside one cell, or below split_min_span): the unsplit build, no cell tests
+        if (np != (uint64_t)mp) {
+            m = np;
+            TRY(gvrt_dalloc(c, (void**)&pbox, 24ull * m));
+            TRY(gvrt_dalloc(c, (void**)&paux, 16ull * m));
+            hipLaunchKernelGGL(k_piece_emit, dim3(pb), dim3(256), 0, c->stream, (uint64_t)mp, c->d_boxes_c, g,
+                               ap.split_min_span, c->box_pad_abs, poff, pbox, paux);
+            TRYH(hipGetLastError(), "k_piece_emit");
+            boxes_in = pbox;
+            c->split_cells = ap.split_cells;
+            for (int a = 0; a < 3; ++a) {
+                c->grid_min[a] = g.mn[a];
+                c->grid_n[a] = g.n[a];
+            }
+            c->grid_inv = g.inv;
         }
-        c->grid_inv = g.inv;
         gvrt_dfree(c, (void**)&bnd);
         gvrt_dfree(c, (void**)&bpart);
     }
@@ -901,8 +943,8 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
 
     const int64_t ninternal = m > 1 ? m - 1 : 1;
     TRY(gvrt_dalloc(c, (void**)&c->d_recs, sizeof(RenderRec) * m));
-    if (!c->split_cells) TRY(gvrt_dalloc(c, (void**)&c->d_sh, 192ull * m));
-    else TRY(gvrt_dalloc(c, (void**)&c->d_leaf_aux, 16ull * m));
+    TRY(gvrt_dalloc(c, (void**)&c->d_sh, 192ull * m));
+    if (c->split_cells) TRY(gvrt_dalloc(c, (void**)&c->d_leaf_aux, 16ull * m));
     TRY(gvrt_dalloc(c, (void**)&c->d_nodes, sizeof(BvhNode) * ninternal));
     TRY(gvrt_dalloc(c, (void**)&c->d_leaf_src, 4ull * m));
 
@@ -1062,6 +1104,11 @@ gvrt_status gvrt_launch_build_accel(gvrt_context* c, const gvrt_accel_params& ap
             c->depth4 = hc[0] + 1;
             c->n_nodes4 = total;
         }
+    }
+    if (c->split_cells && c->n_nodes4 && c->d_leaf_aux) {
+        hipLaunchKernelGGL(k_mark_pieces, dim3((unsigned)((c->n_nodes4 + 255) / 256)), dim3(256), 0, c->stream,
+                           (uint64_t)c->n_nodes4, c->d_nodes4, reinterpret_cast<const uint4*>(c->d_leaf_aux));
+        TRYH(hipGetLastError(), "k_mark_pieces");
     }
     TRYH(hipEventRecord(c->ev1, c->stream), "event");
     TRYH(hipStreamSynchronize(c->stream), "sync");

@@ -400,7 +400,7 @@ __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlan
 // One leaf (record li) for the lanes in bk: response, icosahedron clip, k-buffer insertion.  A macro (as a lambda
 // capturing the k-buffer by reference the kernel spilled 8 B per lane); round 4's wide-node traversal expanded it
 // too (commit f850e68).
-#define GVRT_LEAF(LI_, BK_)                                                                                        \
+#define GVRT_LEAF(LI_, BK_, PIECE_)                                                                                \
     {                                                                                                              \
         const int32_t li = (LI_);                                                                                  \
         const uint64_t bk = (BK_);                                                                                 \
@@ -410,9 +410,9 @@ __device__ inline int32_t unii(int32_t v) { return __builtin_amdgcn_readfirstlan
                                                                                                                    \
         /* split (SplitBLAS analogue): the piece's proxy id and cell; cell == ~0u admits every crossing */         \
         uint4 pa = make_uint4((uint32_t)li, 0xFFFFFFFFu, 0u, 0u);                                                  \
-        if (aux_) pa = aux_[li];                                                                                   \
+        if (PIECE_) pa = aux_[li]; /* a split piece (node mark): its cell */                                       \
         {                                                                                                          \
-            const uint32_t gi = uni(pa.x);                                                                         \
+            const uint32_t gi = (uint32_t)li; /* payload: the leaf (per-leaf records and SH, pieces too) */      \
             wadd(W_LEAVES, 1);                                                                                     \
             if (__builtin_amdgcn_inverse_ballot_w64(bk)) {  /* exec &= bk: no per-lane bit test */                 \
                 ladd(L_LEAVES);                                                                                    \
@@ -788,7 +788,8 @@ __global__ __launch_bounds__(64, RENDER_MIN_WAVES) void k_render(const RenderArg
             while (leafmask) {
                 const int k = __builtin_ctz(leafmask);
                 leafmask &= leafmask - 1;
-                GVRT_LEAF(~GVRT_PICK(ch, k), GVRT_PICK(bal, k))  // leaf slot, lanes whose ray hits its box
+                // leaf slot, lanes whose ray hits its box, and whether it is a split piece (pad[1] bit 4 + k)
+                GVRT_LEAF(~GVRT_PICK(ch, k), GVRT_PICK(bal, k), (inner >> (4 + k)) & 1u)
             }
             if constexpr (STATS) wadd(C_LEAF, __builtin_amdgcn_s_memtime() - s_tph[1]);
             if (next < 0) break;
@@ -1346,6 +1347,7 @@ __device__ inline void set_empty(Bvh4Node& n, int k) {
 struct AcceptArgs {
     float min_response, alpha_min, kmin, kdeg, pad_abs;
     uint32_t kopts;
+    uint32_t split;  // leaves are split pieces (gvrt_accel_params.split_cells)
 };
 
 __global__ __launch_bounds__(256) void k_accept_leaf(uint64_t n, const Bvh4Node* __restrict__ src,
@@ -1357,7 +1359,7 @@ __global__ __launch_bounds__(256) void k_accept_leaf(uint64_t n, const Bvh4Node*
     float dmax = 0.0f;
     // a node with inner children keeps its leaves' proxy boxes (D = 0 would not cover the acceptance boxes, and a
     // D > 0 would widen the inner children's range too); only never-accepted leaves are dropped there
-    const bool all_leaves = nd.pad[1] == 0u;
+    const bool all_leaves = (nd.pad[1] & 0xFu) == 0u;
 #pragma unroll
     for (int k = 0; k < BVH_W; ++k) {
         if (slot_empty(nd, k) || nd.child[k] >= 0) continue;
@@ -1392,7 +1394,29 @@ __global__ __launch_bounds__(256) void k_accept_leaf(uint64_t n, const Bvh4Node*
         // the icosahedron the render kernel clips against: inradius kS (kernel_scale with the enclosing options)
         const float rc = ICO_CIRCUM * 1.001f * kernel_scale(rho, p.kmin, p.kopts, p.kdeg);
         const float gap = sqrtf(fmaxf(rc * rc - re * re, 0.0f));
-        dmax = fmaxf(dmax, gap * fmaxf(sx, fmaxf(sy, sz)) * 1.01f + 4.0f * p.pad_abs);
+        const float dk = gap * fmaxf(sx, fmaxf(sy, sz)) * 1.01f + 4.0f * p.pad_abs;
+        if (p.split) {
+            // a piece admits only the crossings whose point lies in its box (the proxy's box clipped to its cell):
+            // the line's point in E lies within dk of such a crossing, so E's box meets the piece's box grown by dk
+            // (+ its own padding); a piece whose cell E cannot reach that way never admits an accepted crossing
+            bool empty = false;
+            const Bvh4Node& sn = src[i];
+#pragma unroll
+            for (int ax = 0; ax < 3; ++ax) {
+                const float plo = sn.box[k][2 * ax], phi = sn.box[k][2 * ax + 1];
+                const float pad = 1e-5f * (phi - plo + 2.0f * dk) + 1e-6f * fmaxf(fabsf(plo), fabsf(phi)) + p.pad_abs;
+                const float lo = fmaxf(nd.box[k][2 * ax], plo - dk - pad);
+                const float hi = fminf(nd.box[k][2 * ax + 1], phi + dk + pad);
+                nd.box[k][2 * ax] = lo;
+                nd.box[k][2 * ax + 1] = hi;
+                empty = empty || !(lo <= hi);
+            }
+            if (empty) {
+                set_empty(nd, k);
+                continue;
+            }
+        }
+        dmax = fmaxf(dmax, dk);
     }
     nd.pad[2] = __float_as_uint(dmax);
     dst[i] = nd;
@@ -1401,7 +1425,7 @@ __global__ __launch_bounds__(256) void k_accept_leaf(uint64_t n, const Bvh4Node*
 gvrt_status gvrt_launch_accept_nodes(gvrt_context* c, float min_response, float alpha_min) {
     const uint64_t n = c->n_nodes4;
     c->accept_ok = false;
-    if (!n || !c->d_nodes4 || c->split_cells) return GVRT_OK;
+    if (!n || !c->d_nodes4) return GVRT_OK;
     if (!c->d_nodes4e) {
         // without the memory FAST launches keep the proxy-box nodes (no retry until the next build)
         if (c->accept_nomem) return GVRT_OK;
@@ -1419,6 +1443,7 @@ gvrt_status gvrt_launch_accept_nodes(gvrt_context* c, float min_response, float 
     p.kdeg = c->enc.degree;
     p.kopts = c->enc.opts;
     p.pad_abs = c->box_pad_abs;
+    p.split = c->split_cells ? 1u : 0u;
     hipLaunchKernelGGL(k_accept_leaf, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, n, c->d_nodes4,
                        c->d_recs, p, c->d_nodes4e);
     if (c->d_nodes4ex8)

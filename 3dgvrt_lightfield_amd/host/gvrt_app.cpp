@@ -90,7 +90,7 @@ int usage() {
     std::fprintf(stderr,
                  "usage: gvrt_app {render|eval|lightfield|hitcounts|bench|split|views|tiles|cameras|png} [--ply P] [--out D]\n"
                  "       [--width W] [--height H] [--camera orbit|config1] [--variant rq|rt] [--transforms T]\n"
-                 "       [--duration S] [--warmup S] [--frametimes] [--split-cells N] [--build fast|quality]\n"
+                 "       [--duration S] [--warmup S] [--frametimes] [--split-cells N] [--split-min-span N] [--build fast|quality]\n"
                  "       [--device I] [--rank R --world N --id-file F --frames K --layout cost-bands|blocks|views --views V]\n"
                  "       [--costs c0,c1,... (views)]\n");
     return 2;
@@ -199,8 +199,12 @@ int main(int argc, char** argv) {
         }
         gvrt_accel_params ap;
         gvrt_default_accel_params(&ap);
-        ap.split_cells = (uint32_t)std::atoi(a.get("split-cells", "0").c_str());
-        if (a.get("build", "fast") == "quality") {  // static-scene build: device binned SAH + SAH-optimal collapse
+        const bool quality = a.get("build", "fast") == "quality";
+        // quality (static-scene) build: device binned SAH + SAH-optimal collapse, and the SplitBLAS grid (10 cells,
+        // base/Define.h:45-47) applied to the proxies that span 3+ cells (renderer.QUALITY_BUILD in Python)
+        ap.split_cells = (uint32_t)std::atoi(a.get("split-cells", quality ? "10" : "0").c_str());
+        ap.split_min_span = (uint32_t)std::atoi(a.get("split-min-span", quality ? "3" : "0").c_str());
+        if (quality) {
             ap.builder = 2;
             ap.collapse = 1;
         }

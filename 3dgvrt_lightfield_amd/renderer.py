@@ -17,6 +17,13 @@ from ._lib import check, lib
 
 SPLAT_KEYS = (("positions", 3), ("f_dc", 3), ("f_rest", 45), ("opacity", 1), ("scale", 3), ("rotation", 4))
 
+# The static-scene build the bench renders with (Renderer.prepare / build_accel keywords): the device binned-SAH
+# tree with the SAH-optimal 4-wide collapse (the reference's PREFER_FAST_TRACE BLAS, VulkanFullRT.cpp:621) and
+# the SplitBLAS grid of the reference (SPLIT_BLAS, NUMBER_OF_CELLS_PER_LONGEST_AXIS = 10, base/Define.h:45-47)
+# applied to the large proxies only: those whose box overlaps at least 3 cells along an axis (a fifth of the
+# scene) are split into cell pieces, the rest stay whole, and a scene without such proxies gets the unsplit tree.
+QUALITY_BUILD = dict(builder=2, collapse=1, split_cells=10, split_min_span=3)
+
 
 class SplatSet(dict):
     """vk3DGRT::SplatSet: SoA float32 arrays keyed like the C++ members."""
@@ -123,18 +130,18 @@ class Renderer:
             out["verts"], out["tris"] = verts, tris
         return out
 
-    def build_accel(self, split_cells=0, builder=0, collapse=0, depth_budget=0):
+    def build_accel(self, split_cells=0, builder=0, collapse=0, depth_budget=0, split_min_span=0):
         p = _lib.AccelParams()
         lib().gvrt_default_accel_params(C.byref(p))
         p.split_cells, p.builder, p.collapse = int(split_cells), int(builder), int(collapse)
-        p.depth_budget = int(depth_budget)
+        p.depth_budget, p.split_min_span = int(depth_budget), int(split_min_span)
         check(lib().gvrt_build_accel_ex(self.h, C.byref(p)), self.h)
 
-    def prepare(self, splats, split_cells=0, builder=0, collapse=0, **enclosing):
+    def prepare(self, splats, split_cells=0, builder=0, collapse=0, split_min_span=0, **enclosing):
         """VulkanFullRT::prepare: upload, enclose, build the acceleration structure."""
         self.load_splats(splats)
         m = self.build_enclosing(**enclosing)
-        self.build_accel(split_cells=split_cells, builder=builder, collapse=collapse)
+        self.build_accel(split_cells=split_cells, builder=builder, collapse=collapse, split_min_span=split_min_span)
         return m
 
     def set_option(self, name, value):

@@ -6,7 +6,8 @@ Workload at N=1: config 2 ("bicycle" stand-in, 1M synthetic Gaussians, seed 1, 1
 camera r=4 / elev 20 / fovy 50, ray-query variant).  A step = one Particle Rendering pass over one
 1920x1080 view with the scene, proxies and BVH resident in HBM (enclosing + BVH build are
 one-shot and reported separately; by default the static-scene quality build on the device (binned SAH +
-SAH-optimal collapse, ~9 ms at 1M), `--build fast` for the ~1.5 ms device LBVH).
+SAH-optimal collapse, ~9 ms at 1M, with the reference's SplitBLAS grid applied to proxies spanning 3+ of its 10
+cells: renderer.QUALITY_BUILD), `--build fast` for the ~1.5 ms device LBVH).
 
 Several GPUs: `python bench.py --gpus N` started as one process launches its N ranks
 itself (torch.distributed.run, one process per GPU; dist.launch_ranks); launched by torch.distributed.run
@@ -99,7 +100,7 @@ def parse():
                     help="N-rank runs: a strong-scaling sub-record starts only while the run's wall time is below this "
                          "(rank 0 decides, every rank follows); later ones are listed as skipped, so the line still prints")
     ap.add_argument("--build", default="quality", choices=["quality", "fast"],
-                    help="quality: device binned-SAH tree + SAH-optimal 4-wide collapse (the static-scene build, "
+                    help="quality: device binned-SAH tree + SAH-optimal 4-wide collapse + large-proxy SplitBLAS pieces (the static-scene build, "
                          "as the reference's PREFER_FAST_TRACE BLAS); fast: device LBVH + greedy collapse")
     args = ap.parse_args()
     if args.split == "auto":
@@ -603,7 +604,7 @@ def main():
     if args.configs_child:  # the configs record's PMC child: render CONFIG_SET, print the launch manifest
         import torch
         gv = importlib.import_module("3dgvrt_lightfield_amd")
-        bkw = dict(builder=2, collapse=1) if args.build == "quality" else {}
+        bkw = dict(gv.QUALITY_BUILD) if args.build == "quality" else {}
         _, manifest = run_config_set(gv, torch, args.steps, args.warmup, literal=False, bkw=bkw)
         print(json.dumps({"manifest": manifest}), flush=True)
         return
@@ -647,7 +648,7 @@ def main():
     for kv in args.option:
         name, _, val = kv.partition("=")
         r.set_option(name, int(val))
-    bkw = dict(builder=2, collapse=1) if args.build == "quality" else {}
+    bkw = dict(gv.QUALITY_BUILD) if args.build == "quality" else {}
     m = r.prepare(splats, **bkw)
     first_build = r.stats()  # includes the one-time lazy loading of the build kernels' code objects
     m = r.prepare(splats, **bkw)    # steady-state scene build (what a scene change costs)
@@ -1108,7 +1109,8 @@ def main():
                        "dispatch": "tiles costliest-first by the previous frame's per-tile cost, each cost class "
                                    "dealt to the 8 XCDs in contiguous chunks (handle options tile_order=0: supertile order; "
                                    "tile_xcd=0: no dealing)",
-                       "build": ("quality: device binned-SAH tree + SAH-optimal 4-wide collapse" if args.build == "quality"
+                       "build": ("quality: device binned-SAH tree + SAH-optimal 4-wide collapse, proxies spanning 3+ "
+                                 "of 10 SplitBLAS cells split into cell pieces" if args.build == "quality"
                                  else "fast: device LBVH + greedy 4-wide collapse")},
             "fps": round(1e3 / ms_per_step, 2),
             "kernel_ms": round(kern_avg, 4),

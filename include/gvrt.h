@@ -170,13 +170,20 @@ gvrt_status gvrt_read_enclosing(gvrt_handle h, float* density12, float* sh48, fl
  * finish within it halves the Morton-ordered range instead), and an LBVH or PLOC tree too deep for the
  * stack is rebuilt by the device SAH build (the Vulkan driver's BVH never refuses a scene either).
  * depth_budget: 0 = the default budget (43 binary levels, i.e. at most 42 4-wide levels); smaller values
- * (>= 1 + ceil(log2 survivors)) tighten it for tests of the budget path. */
+ * (>= 1 + ceil(log2 survivors)) tighten it for tests of the budget path.  split_min_span (with
+ * split_cells): a proxy is split only when its box overlaps at least this many cells along one axis,
+ * smaller ones stay whole (one piece admitting every crossing); 0-2 = every proxy that overlaps more
+ * than one cell (the reference's rule), at most 1023.  A split that splits no proxy is the unsplit
+ * build (gvrt_stats.bvh_leaves = survivors).  Pieces keep every per-leaf path of the unsplit tree
+ * (acceptance boxes, kernel-frame origin records, exact boxes); a leaf that is a piece costs one more
+ * 16-B load per visit. */
 typedef struct {
     uint32_t split_cells;
     uint32_t builder;
     uint32_t collapse;
     uint32_t depth_budget;
-    uint32_t reserved[4];
+    uint32_t split_min_span;
+    uint32_t reserved[3];
 } gvrt_accel_params;
 
 void gvrt_default_accel_params(gvrt_accel_params* p);

@@ -2,7 +2,7 @@
 
 A variant is 'default' (the in-tree libgvrt.so), a build name ('3dgvrt_lightfield_amd/build/<name>/libgvrt.so'),
 or 'name:key=v,key2=w' (the in-tree library with handle options, gvrt_set_option by name, e.g. tile_order=0,
-or environment settings such as AB_K=16 for the k-buffer depth; 'lib@name:key=v' both).  One child process
+or environment settings such as AB_K=16 for the k-buffer depth, AB_SPLIT=10 for split_cells, AB_SPAN=3 for split_min_span; 'lib@name:key=v' both).  One child process
 per variant; FAST mode, median kernel ms of 15 renders; each frame is compared with the first variant's
 (max |d rgba| and the count of pixels differing by more than 1e-4)."""
 import json
@@ -29,7 +29,8 @@ k = int(os.environ.get("AB_K", "0"))
 with gv.Renderer(0) as r:
     for name, val in opts.items():
         r.set_option(name, val)
-    r.prepare(s, builder=2, collapse=1)
+    r.prepare(s, builder=2, collapse=1, split_cells=int(os.environ.get("AB_SPLIT", "0")),
+              split_min_span=int(os.environ.get("AB_SPAN", "0")))
     img = r.render(vi, pi, W, H, kbuffer_depth=k, rgba8=False)["rgba32f"]
     np.save(outp, img)
     r.set_stats(True)

@@ -27,7 +27,7 @@ def main():
     gen, W, H, _ = gv.scene.CONFIGS[cfg]
     s = gv.scene.make(**gen)
     with gv.Renderer(0) as r:
-        r.prepare(s, builder=2, collapse=1)
+        r.prepare(s, **gv.QUALITY_BUILD)
         c0, ms0 = classes(r, 30.0, W, H)
         c0b, _ = classes(r, 30.0, W, H)
         out["static"], out["static_repeat"], out["static_ms"] = c0, c0b, ms0

@@ -13,7 +13,7 @@ with gv.Renderer(0) as r:
     for name, val in opts:  # per-handle options (same-binary A/B), e.g. GVRT_OPTS=compact_nodes=1
         r.set_option(name, int(val))
     # the bench's default quality build (GVRT_BUILD=fast: device LBVH)
-    r.prepare(s, **({} if os.environ.get("GVRT_BUILD") == "fast" else dict(builder=2, collapse=1)))
+    r.prepare(s, **({} if os.environ.get("GVRT_BUILD") == "fast" else dict(gv.QUALITY_BUILD)))
     for _ in range(n):
         r.render(vi, pi, W, H, kbuffer_depth=k, rgba8=False, rgba32f=False)
     print("render_ms", r.stats()["render_ms"])

@@ -146,7 +146,8 @@ def test_dense_standin(gv, O):
     splats, W, H, _ = _scene(gv, "dense")
     vi, pi = gv.scene.mipnerf_camera(W, H)
     with gv.Renderer(0) as r:
-        m = r.prepare(splats)
+        m = r.prepare(splats, **gv.QUALITY_BUILD)  # the bench's build: its largest proxies split into cell pieces
+        assert r.stats()["bvh_leaves"] > m
         fast = r.render(vi, pi, W, H, hit_counts=True)
         lit = r.render(vi, pi, W, H, mode=gv.MODE_LITERAL)
     m_ref, sub, ref, sc = _oracle_subset(O, splats, vi, pi, W, H, stride=2)

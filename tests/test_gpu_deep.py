@@ -89,7 +89,8 @@ def test_trained_standin_vs_oracle(gv, O):
     splats = gv.scene.make(**gen)
     vi, pi = gv.scene.mipnerf_camera(W, H)
     with gv.Renderer(0) as r:
-        m = r.prepare(splats, builder=2, collapse=1)  # the bench's quality build
+        m = r.prepare(splats, **gv.QUALITY_BUILD)  # the bench's quality build: its giants are split into cell pieces
+        assert r.stats()["bvh_leaves"] > m
         fast = r.render(vi, pi, W, H, hit_counts=True)
         again = r.render(vi, pi, W, H)
         lit = r.render(vi, pi, W, H, mode=gv.MODE_LITERAL)

@@ -6,7 +6,10 @@ step fails here, at 1080p and 1-3 M Gaussians, where the oracle comparisons only
 The second, cost-ordered launch of the same frame is pinned too (dispatch order changes no pixel).
 Round 5 made 32 slots the FAST default: the 24-slot frames keep their round-1 / round-2 pins (kbuffer_depth = 24)
 and the default frames have their own (a different depth moves the round boundaries, so a ray with a
-flagged tie or threshold decision, DESIGN.md §5, may land on its other side)."""
+flagged tie or threshold decision, DESIGN.md §5, may land on its other side).  Round 6 made the bench's build
+renderer.QUALITY_BUILD (the proxies spanning 3+ of 10 SplitBLAS cells split into pieces): bicycle and garden have
+no such proxy or render the same frame, the dense stand-in's pieces move its tie rays, so the quality build has
+its own pins beside the unsplit SAH build's."""
 import hashlib
 
 import numpy as np
@@ -28,9 +31,19 @@ DIGESTS = {
 }
 
 
+QUALITY_DIGESTS = {  # renderer.QUALITY_BUILD, the default depth
+    "bicycle": "bf93e792aa2149fdb1304de3f77bd38ea57e7a89",
+    "garden": "d9cd8b7420b7f17a2a067509717d800dad0ec558",
+    "dense": "5e3390d8862727b930f950b0d91f8588c4a2a52a",  # its pieces move tie rays (round 6)
+}
+
+
+@pytest.mark.parametrize("build", ["sah", "quality"])
 @pytest.mark.parametrize("depth", sorted(DIGESTS))
 @pytest.mark.parametrize("cfg", sorted(DIGESTS[24]))
-def test_bench_frame_digest(gv, cfg, depth):
+def test_bench_frame_digest(gv, cfg, depth, build):
+    if build == "quality" and depth != 0:
+        pytest.skip("the quality build is pinned at the default depth")
     gen, W, H, _ = gv.scene.CONFIGS[cfg]
     splats = gv.scene.make(**gen)
     # bench.py: a one-view planar rig at the config camera (orbit r 4, elevation 20, azimuth 30, fovy 50)
@@ -39,12 +52,12 @@ def test_bench_frame_digest(gv, cfg, depth):
                                             fovy_deg=50.0, aspect=gv.camera.aspect_ratio(W, H), centred=False)
     vi = np.ascontiguousarray(vis.reshape(1, 16)[0])
     with gv.Renderer(0) as r:
-        r.prepare(splats, builder=2, collapse=1)
+        r.prepare(splats, **(dict(builder=2, collapse=1) if build == "sah" else gv.QUALITY_BUILD))
         params = r.render_params(mode=gv.MODE_FAST, kbuffer_depth=depth)
         first = r.render(vi, pi, W, H, 1, params=params, rgba32f=False)["rgba8"]
         ordered = r.render(vi, pi, W, H, 1, params=params, rgba32f=False)["rgba8"]
     assert first.shape == (1, H, W, 4)
     np.testing.assert_array_equal(ordered, first)
     digest = hashlib.sha1(first[0].tobytes()).hexdigest()
-    print(f"digest {cfg} depth {depth}: {digest}")
-    assert digest == DIGESTS[depth][cfg]
+    print(f"digest {cfg} depth {depth} build {build}: {digest}")
+    assert digest == (DIGESTS[depth][cfg] if build == "sah" else QUALITY_DIGESTS[cfg])

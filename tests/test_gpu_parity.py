@@ -566,7 +566,8 @@ def test_bicycle_full_frame_vs_oracle_and_fast_literal(gv, O, bicycle):
     W, H = 1920, 1080
     vi, pi = gv.scene.mipnerf_camera(W, H)
     with gv.Renderer(0) as r:
-        m = r.prepare(bicycle, builder=2, collapse=1)  # the bench's quality build
+        m = r.prepare(bicycle, **gv.QUALITY_BUILD)  # the bench's quality build (no proxy large enough to split)
+        assert r.stats()["bvh_leaves"] == m
         fast = r.render(vi, pi, W, H)
         lit = r.render(vi, pi, W, H, mode=gv.MODE_LITERAL)
         again = r.render(vi, pi, W, H)

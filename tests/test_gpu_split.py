@@ -50,6 +50,47 @@ def test_split_config1_equals_unsplit(gv, O, config1, config1_enc, cells):
     _cmp_images(out["rgba32f"], ref)
 
 
+@pytest.mark.parametrize("cells,span", [(40, 3), (40, 8), (10, 2)])
+def test_split_min_span_equals_unsplit(gv, O, config1, config1_enc, cells, span):
+    """Size-selective split (gvrt_accel_params.split_min_span): only proxies whose box overlaps at least `span` cells
+    along one axis are split, the others stay one piece admitting every crossing -- fewer pieces than the
+    reference's rule (span <= 2: every straddler, the same tree as split_min_span = 0), the same image."""
+    W = H = 160
+    vi, pi = gv.scene.config1_camera(W, H)
+    with gv.Renderer(0) as r:
+        m = r.prepare(config1)
+        base = r.render(vi, pi, W, H, hit_counts=True)
+        r.build_accel(split_cells=cells)
+        every = r.stats()["bvh_leaves"]
+        r.build_accel(split_cells=cells, split_min_span=span)
+        some = r.stats()["bvh_leaves"]
+        out = r.render(vi, pi, W, H, hit_counts=True)
+        if span <= 2:
+            assert some == every
+        else:
+            assert m < some < every
+        _close(out["rgba32f"], base["rgba32f"])
+        assert (out["hit_counts"] != base["hit_counts"]).mean() <= 1e-4
+        with pytest.raises(gv.GvrtError):
+            r.build_accel(split_cells=cells, split_min_span=1024)
+    _cmp_images(out["rgba32f"], O.render(config1_enc, vi, pi, W, H, proxy_mode=1))
+
+
+def test_split_without_pieces_is_the_unsplit_build(gv, config1):
+    """A split that splits no proxy (split_min_span above every proxy's span) builds the unsplit tree: the same
+    4-wide nodes word for word, no cell tests, the same frame."""
+    W = H = 96
+    vi, pi = gv.scene.config1_camera(W, H)
+    with gv.Renderer(0) as r:
+        m = r.prepare(config1, builder=2, collapse=1)
+        tree = r.read_accel(1)
+        img = r.render(vi, pi, W, H)["rgba32f"]
+        r.build_accel(builder=2, collapse=1, split_cells=10, split_min_span=1023)
+        assert r.stats()["bvh_leaves"] == m
+        np.testing.assert_array_equal(r.read_accel(1), tree)
+        np.testing.assert_array_equal(r.render(vi, pi, W, H)["rgba32f"], img)
+
+
 def test_split_bicycle_vs_oracle(gv, O):
     splats = gv.scene.mipnerf_standin(1_000_000, seed=1)
     W, H = 1920, 1080
