@@ -48,7 +48,9 @@ with gv.Renderer(0) as r:
                       "nodes/wave": round(st["wave_node_visits"] / waves, 1),
                       "leaves/wave": round(st["wave_leaf_visits"] / waves, 1),
                       "rounds/wave": round(st["wave_rounds"] / waves, 3),
-                      "flushes/wave": round(st.get("wave_flushes", 0) / waves, 2)}))
+                      "flushes/wave": round(st.get("wave_flushes", 0) / waves, 2),
+                      "leaf_lane_util": round(st["lane_leaf_tests"] / max(64 * st["wave_leaf_visits"], 1), 3),
+                      "dead_node_frac": round(st["wave_dead_visits"] / max(st["wave_node_visits"], 1), 3)}))
 ''' % ROOT
 
 cfg = sys.argv[1]

@@ -184,6 +184,31 @@ def test_cost_ordered_dispatch_changes_no_pixel(gv, config1):
                                           first["rgba32f"][0][8 * ty:8 * ty + 8, 8 * tx:8 * tx + 8])
 
 
+def test_duplicate_tile_list_then_moving_camera(gv, config1):
+    """a caller's tile list with duplicates and at least as many entries as the frame has tiles
+    must not leave cells of the dilation grid unwritten (the grid is cleared unless the list is the handle's own
+    full-frame list; classes are clamped to TILE_BUCKETS - 1).  The frames of a moving camera after such a list
+    equal a fresh handle's frames of the same cameras, bit for bit."""
+    W, H = 72, 40  # 9 x 5 = 45 tiles
+    eyes = [gv.camera.orbit_eye(3.0, 15.0, 30.0 + 2.0 * k) for k in range(4)]
+    cams = [gv.camera.pinhole(e, (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 45.0, gv.camera.aspect_ratio(W, H)) for e in eyes]
+    dup = [(0, 0, 0, 0)] * 20 + [(tx, ty, 0, 0) for ty in range(5) for tx in range(9)] + [(8, 4, 0, 0)] * 7
+    t = np.asarray(dup, np.uint16)
+    assert len(t) >= 45
+    with gv.Renderer(0) as r, gv.Renderer(0) as fresh:
+        r.prepare(config1)
+        fresh.prepare(config1)
+        vi0, pi0 = cams[0]
+        full0 = r.render(vi0, pi0, W, H)["rgba32f"]
+        part = r.render(vi0, pi0, W, H, tiles=t)["rgba32f"]
+        np.testing.assert_array_equal(part, full0)  # every tile listed, some twice: the same pixels
+        for vi, pi in cams[1:]:  # moving camera: each launch dilates the previous classes by its motion
+            got = r.render(vi, pi, W, H, hit_counts=True)
+            want = fresh.render(vi, pi, W, H, hit_counts=True)
+            for k in ("rgba32f", "rgba8", "hit_counts"):
+                np.testing.assert_array_equal(got[k], want[k])
+
+
 def test_record_origin_prep_changes_no_pixel(gv, config1):
     """Single-origin FAST launches read each leaf's kernel-frame origin from its record (k_rec_origin writes it
     per launch in place of the position; other launches get the positions back, k_rec_restore).  Frames agree
