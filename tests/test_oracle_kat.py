@@ -286,7 +286,7 @@ def mipnerf_small(gv, O):
 @pytest.mark.parametrize("ulps", [1, 2, 4])
 def test_conditioning_flags_cover_another_float_evaluation(gv, O, mipnerf_small, ulps):
     """the unflagged rays that differed from the GPU by more than 1e-4 (bicycle 6, light field 2, dense
-    1; scripts/parity_outliers.py) were a particle's pair of crossings whose response lay 1.05-1.45e-4 from
+    1; tests/tools/parity_outliers.py) were a particle's pair of crossings whose response lay 1.05-1.45e-4 from
     hitMinGaussianResponse with a relative float uncertainty of the same size (|gro| of 200-400: the line's distance
     from the centre is a difference of products ~|gro|), and, on the dense scene, two composited crossings 6.8e-6 apart
     in t while a face crossed at grazing incidence makes t uncertain by more.  The oracle now flags a decision within

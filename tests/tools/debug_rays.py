@@ -1,5 +1,5 @@
 """Debug: chosen rays of a bench configuration, GPU (FAST, LITERAL, with hit counts) next to the oracle (its
-per-crossing trace, margins and flip bound).  python scripts/debug_rays.py <config> <ray index>...  (quality
+per-crossing trace, margins and flip bound).  python tests/tools/debug_rays.py <config> <ray index>...  (quality
 build, the bench camera); prints one JSON record per ray."""
 import importlib
 import json
@@ -8,7 +8,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 gv = importlib.import_module("3dgvrt_lightfield_amd")

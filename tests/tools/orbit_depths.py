@@ -1,5 +1,10 @@
+"""Test-infrastructure model (CPU oracle): per-tile depths of the bicycle stand-in's tile-centre rays and a
+reprojected dispatch order scored against the round-4 orbit cost dumps (profiles/EXPERIMENTS.md round 6).
+usage: python tests/tools/orbit_depths.py bicycle && python tests/tools/orbit_reproject_model.py bicycle"""
+import os
+_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import sys, importlib, numpy as np
-sys.path.insert(0,'/root/repo'); sys.path.insert(0,'/root/repo/oracle'); sys.path.insert(0,'/root/repo/scripts')
+sys.path.insert(0,_ROOT); sys.path.insert(0,os.path.join(_ROOT,'oracle'))
 gv=importlib.import_module("3dgvrt_lightfield_amd"); import oracle as O
 from scipy.ndimage import maximum_filter
 import heapq
@@ -14,7 +19,7 @@ def score(cost, proxy):
     proxy=proxy.reshape(-1); order=np.argsort(-proxy,kind="stable"); bound=max(cost.sum()/SLOTS,cost.max())
     return round(float(np.corrcoef(rank(proxy),rank(cost))[0,1]),3), round(makespan(cost[order])/bound,4)
 cfg=sys.argv[1]
-d=np.load('/root/repo/profiles/r04/orbit_costs_%s.npz'%cfg)
+d=np.load(os.path.join(_ROOT,'profiles')+'/r04/orbit_costs_%s.npz'%cfg)
 gen,W,H,_=gv.scene.CONFIGS[cfg]; s=gv.scene.make(**gen)
 TX,TY=W//8,H//8
 vi0,pi0=gv.scene.mipnerf_camera(W,H,azimuth_deg=30.0)
@@ -37,4 +42,4 @@ for i,ray in enumerate(rays):
     zs[i]=(t*w).sum()/max(w.sum(),1e-6) if w.sum()>1e-4 else np.median(t)
     zmed[i]=np.median(t)
 print('traced', time.time()-t0)
-np.savez('/tmp/lf/depth_%s.npz'%cfg, zs=zs, zmed=zmed, dirs=dirs)
+np.savez('/tmp/orbit_depth_%s.npz'%cfg, zs=zs, zmed=zmed, dirs=dirs)

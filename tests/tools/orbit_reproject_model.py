@@ -1,5 +1,10 @@
+"""Test-infrastructure model (CPU oracle): per-tile depths of the bicycle stand-in's tile-centre rays and a
+reprojected dispatch order scored against the round-4 orbit cost dumps (profiles/EXPERIMENTS.md round 6).
+usage: python tests/tools/orbit_depths.py bicycle && python tests/tools/orbit_reproject_model.py bicycle"""
+import os
+_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import sys, importlib, numpy as np, heapq
-sys.path.insert(0,'/root/repo')
+sys.path.insert(0,_ROOT)
 gv=importlib.import_module("3dgvrt_lightfield_amd")
 from scipy.ndimage import maximum_filter
 SLOTS=4096
@@ -13,8 +18,8 @@ def score(cost, proxy):
     proxy=proxy.reshape(-1); order=np.argsort(-proxy,kind="stable"); bound=max(cost.sum()/SLOTS,cost.max())
     return round(float(np.corrcoef(rank(proxy),rank(cost))[0,1]),3), round(makespan(cost[order])/bound,4)
 cfg=sys.argv[1]
-d=np.load('/root/repo/profiles/r04/orbit_costs_%s.npz'%cfg)
-z=np.load('/tmp/lf/depth_%s.npz'%cfg)
+d=np.load(os.path.join(_ROOT,'profiles')+'/r04/orbit_costs_%s.npz'%cfg)
+z=np.load('/tmp/orbit_depth_%s.npz'%cfg)
 gen,W,H,_=gv.scene.CONFIGS[cfg]
 TX,TY=W//8,H//8
 prev=d['static'].astype(np.float64)

@@ -1,7 +1,7 @@
 """Diagnose the off-threshold parity outliers (VERDICT r03 "what's next" #1): rays the oracle does not flag whose
 GPU colour differs from the oracle's by more than 1e-4.
 
-    python scripts/parity_outliers.py <config> [stride] [offset]     (config: bicycle, dense, lightfield, garden)
+    python tests/tools/parity_outliers.py <config> [stride] [offset]     (config: bicycle, dense, lightfield, garden)
 
 Renders the bench view (FAST and LITERAL, hit counts, ray directions) on the GPU, runs the oracle with margins on
 every stride-th ray, and for each unflagged ray beyond 1e-4 prints one JSON record: the two colours, the accepted
@@ -19,7 +19,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 gv = importlib.import_module("3dgvrt_lightfield_amd")
