@@ -216,6 +216,10 @@ class Scene:
         vi = np.ascontiguousarray(view_inv, np.float32).reshape(-1)
         pi = np.ascontiguousarray(proj_inv, np.float32).reshape(16)
         r = np.ascontiguousarray(rays, np.uint64).reshape(-1)
+        if len(r) == 0:
+            z = np.zeros(0, np.float32)
+            return {"dist": z, "kind": z.astype(np.int32), "variants": z.astype(np.int32),
+                    "decisions": z.astype(np.int32), "vbound": z, "alt_rgba": np.zeros((0, 4), np.float32)}
         tg = np.ascontiguousarray(np.asarray(target_rgb, np.float32).reshape(-1, 4)[:, :3]
                                   if np.asarray(target_rgb).reshape(len(r), -1).shape[1] == 4
                                   else np.asarray(target_rgb, np.float32).reshape(-1, 3))
