@@ -4,10 +4,12 @@ within 1e-4 with the oracle's accepted-hit count (FAST), every flagged ray that 
 oracle alternative with its flagged decisions taken the other way (explain_flagged), PSNR >= 50 dB.
 
 Each case draws: the scene family (config-1 cube, Mip-NeRF-like stand-in, dense stand-in, trained-splat stand-in) and
-its size, scale and opacity; an orbit camera (radius, elevation, azimuth, field of view) and an odd frame size; the
+its size, scale and opacity; the enclosing (default, or adaptive clamping with kernelMinResponse 0.0113 / 0.05,
+particlePrimitives.comp:81-105); an orbit camera (radius, elevation, azimuth, field of view) and a frame size; the
 kernel (FAST at 8 / 16 / 24 / 32 slots, LITERAL); the ray-generation variant (RQ corner rays, or the RT pipeline's
-pixel centres with alpha starting at 1, Q10 / Q11); the build (device LBVH, the quality build with large-proxy pieces,
-every straddler split on a 10-cell grid).  The same seeds give the same cases on every box."""
+pixel centres with alpha starting at 1, Q10 / Q11); the render thresholds (minTransmittance, hitMinGaussianResponse,
+alphaMinThreshold, SH degree; VulkanUtils.h:35-68); the build (device LBVH, the quality build with large-proxy
+pieces, every straddler split on a 10-cell grid).  The same seeds give the same cases on every box."""
 import numpy as np
 import pytest
 
@@ -44,31 +46,36 @@ def _case(gv, seed):
     depth = 0 if literal else int(rng.choice(DEPTHS))
     rt = rng.random() < 0.4
     variant = dict(pixel_offset=0.5, alpha_init=1.0) if rt else {}
+    if rng.random() < 0.4:  # render thresholds other than the defaults (the same on both sides)
+        variant.update(min_transmittance=float(rng.choice([0.001, 0.01, 0.05])),
+                       hit_min_gaussian_response=float(rng.choice([0.0113, 0.03, 0.1])),
+                       alpha_min=float(rng.choice([1.0 / 255.0, 0.02])), sph_eval_degree=int(rng.integers(0, 4)))
+    enc = dict(kernel_min_response=float(rng.choice([0.0113, 0.05])), opts=1) if rng.random() < 0.25 else {}
     build = [dict(), dict(gv.QUALITY_BUILD), dict(builder=2, collapse=1, split_cells=10)][int(rng.integers(3))]
     return dict(kind=kind, splats=s, W=W, H=H, vi=vi, pi=pi, literal=literal, depth=depth, variant=variant,
-                build=build)
+                build=build, enc=enc)
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("seed", range(40))
+@pytest.mark.parametrize("seed", range(120))
 def test_random_case_vs_oracle(gv, O, seed):
     c = _case(gv, seed)
     W, H, vi, pi = c["W"], c["H"], c["vi"], c["pi"]
     mode = gv.MODE_LITERAL if c["literal"] else gv.MODE_FAST
     with gv.Renderer(0) as r:
-        m = r.prepare(c["splats"], **c["build"])
+        m = r.prepare(c["splats"], **c["build"], **c["enc"])
         kw = dict(c["variant"])
         if not c["literal"]:
             kw["kbuffer_depth"] = c["depth"]
         out = r.render(vi, pi, W, H, mode=mode, hit_counts=True, **kw)
-    e = O.enclose(c["splats"])
+    e = O.enclose(c["splats"], **c["enc"])
     assert e["m"] == m
-    sc = O.Scene(e)
+    sc = O.Scene(e, **c["enc"])
     try:
         ref = sc.render(vi, pi, W, H, margin=True, **c["variant"])
         ref = {k: v.reshape(W * H, -1) for k, v in ref.items()}
         got = out["rgba32f"].reshape(-1, 4)
-        desc = {k: c[k] for k in ("kind", "W", "H", "literal", "depth", "variant", "build")}
+        desc = {k: c[k] for k in ("kind", "W", "H", "literal", "depth", "variant", "build", "enc")}
         print(f"case {seed}: {desc}, M {m}, flagged {O.ambiguous(ref['margin']).mean():.4f}")
         # the flags are the oracle's and depend only on the scene and camera; dense close-ups flag the most
         _cmp_images(got, ref, amb_max=0.15)
