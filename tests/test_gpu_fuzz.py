@@ -77,8 +77,9 @@ def test_random_case_vs_oracle(gv, O, seed):
         got = out["rgba32f"].reshape(-1, 4)
         desc = {k: c[k] for k in ("kind", "W", "H", "literal", "depth", "variant", "build", "enc")}
         print(f"case {seed}: {desc}, M {m}, flagged {O.ambiguous(ref['margin']).mean():.4f}")
-        # the flags are the oracle's and depend only on the scene and camera; dense close-ups flag the most
-        _cmp_images(got, ref, amb_max=0.15)
+        # the flags are the oracle's and depend only on the scene and camera; dense close-ups and small Gaussians
+        # seen from afar (ill-conditioned values) flag the most: up to 18 % of a case's rays
+        _cmp_images(got, ref, amb_max=0.25)
         if not c["literal"]:
             amb = O.ambiguous(ref["margin"])
             assert (out["hit_counts"].reshape(-1) != ref["stats"][:, 1])[~amb].sum() == 0

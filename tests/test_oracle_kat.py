@@ -303,7 +303,7 @@ def test_conditioning_flags_cover_another_float_evaluation(gv, O, mipnerf_small,
     b = mipnerf_small.render(vi, pi, W, H, perturb_ulps=ulps)
     amb = O.ambiguous(a["margin"])
     fb = O.flip_bound(a["margin"])
-    assert 0.003 < amb.mean() < 0.015, amb.mean()
+    assert 0.003 < amb.mean() < 0.02, amb.mean()  # 1.56 % since the world-space value conditioning (round 6)
     d = np.abs(a["rgba32f"][:, :3] - b["rgba32f"][:, :3]).max(axis=1)
     moved = a["stats"][:, 1] != b["stats"][:, 1]
     assert moved.sum() > 0 and not (moved & ~amb).any()  # decisions move, only on flagged rays
@@ -399,5 +399,26 @@ def test_explain_reproduces_gpu_termination_ties(gv, O):
         ex = sc.explain(vi, pi, W, H, rays, gpu, ncams=ncams)
         assert (ex["kind"] == 1).all() and (ex["dist"] <= 2e-6).all(), ex
         np.testing.assert_array_equal(ex["alt_rgba"][:, 3], gpu[:, 3])
+    finally:
+        sc.close()
+
+
+def test_value_flag_world_space_conditioning(gv, O):
+    """Case 77 of the randomised sweep (tests/test_gpu_fuzz.py): the GPU's value of one ray was 1.2e-4 from the oracle's
+    with no decision near a threshold.  Its first particle is anisotropic (scales 0.004-0.017) and 8 units away: a
+    rounding of the world-space ray reaches its kernel frame amplified by |o - p| / s_min (1860), three times |gro|,
+    which the decision conditioning uses.  The value conditioning now takes the larger, so the ray is flagged and the
+    GPU's value (kept as a fixture) is within 1e-4 plus its value bound of the oracle's march."""
+    import test_gpu_fuzz as F
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "fuzz77_value_r06.json")))
+    c = F._case(gv, fx["seed"])
+    W, H, vi, pi = c["W"], c["H"], c["vi"], c["pi"]
+    sc = O.Scene(O.enclose(c["splats"]))
+    try:
+        ray = np.array([fx["ray"]], np.uint64)
+        ref = sc.render(vi, pi, W, H, subset=ray, margin=True, **c["variant"])
+        assert O.ambiguous(ref["margin"]).all() and ref["margin"][0, 0] == 0.0  # value-flagged
+        ex = sc.explain(vi, pi, W, H, ray, np.array([fx["gpu_rgba"]], np.float32), **c["variant"])
+        assert 1e-4 < ex["dist"][0] <= 1e-4 + ex["vbound"][0], ex
     finally:
         sc.close()
