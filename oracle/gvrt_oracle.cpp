@@ -1320,16 +1320,18 @@ int oracle_scene_explain(void* h, const oracle_params* P, const float* viewInver
         RayOut base;
         marchRay(*os, P, o, d, true, nullptr, &vars, base);
         const float* tg = target + 3 * k;
-        // an alternative explains the target when it lies within tol plus the alternative's own value bound (the
-        // colour its ill-conditioned responses may move, FLAG_VALUE_EPS); the excess over that is what is minimised
+        // an alternative explains the target exactly when it lies within tol; failing that, within tol plus the
+        // alternative's own value bound (the colour its ill-conditioned responses may move, FLAG_VALUE_EPS).  The search
+        // runs until an exact alternative is found (single variants, then pairs) and reports it; otherwise the one
+        // whose excess over its value bound is smallest
         auto dist = [&](const RayOut& ro) {
             float m = 0.0f;
             for (int c = 0; c < 3; ++c) m = std::max(m, std::fabs(ro.rgba[c] - tg[c]));
             return m;
         };
-        float best = dist(base) - base.vbound;
-        int kind = 0;
-        RayOut best_out = base;
+        float best_exact = dist(base), best_rel = dist(base) - base.vbound;
+        int kind_exact = 0, kind_rel = 0;
+        RayOut exact_out = base, rel_out = base;
         uint32_t ngroups = vars.empty() ? 0u : vars.back().group + 1u;
         auto consider = [&](const Variant* v, int nv, int knd) {
             Forced F;
@@ -1337,22 +1339,30 @@ int oracle_scene_explain(void* h, const oracle_params* P, const float* viewInver
             F.n = nv;
             RayOut ro;
             marchRay(*os, P, o, d, true, &F, nullptr, ro);
-            const float dd = dist(ro) - ro.vbound;
-            if (dd < best) {
-                best = dd;
-                kind = knd;
-                best_out = ro;
+            const float dd = dist(ro);
+            if (dd < best_exact) {
+                best_exact = dd;
+                kind_exact = knd;
+                exact_out = ro;
+            }
+            if (dd - ro.vbound < best_rel) {
+                best_rel = dd - ro.vbound;
+                kind_rel = knd;
+                rel_out = ro;
             }
         };
-        for (size_t i = 0; i < vars.size() && best > tol; ++i) consider(&vars[i], 1, 1);
+        for (size_t i = 0; i < vars.size() && best_exact > tol; ++i) consider(&vars[i], 1, 1);
         uint32_t pairs = 0;
-        for (size_t i = 0; i < vars.size() && best > tol && pairs < max_pairs; ++i)
-            for (size_t j = i + 1; j < vars.size() && best > tol && pairs < max_pairs; ++j) {
+        for (size_t i = 0; i < vars.size() && best_exact > tol && pairs < max_pairs; ++i)
+            for (size_t j = i + 1; j < vars.size() && best_exact > tol && pairs < max_pairs; ++j) {
                 if (vars[i].group == vars[j].group) continue;
                 const Variant two[2] = {vars[i], vars[j]};
                 consider(two, 2, 2);
                 ++pairs;
             }
+        const bool exact = best_exact <= tol;
+        const RayOut& best_out = exact ? exact_out : rel_out;
+        const int kind = exact ? kind_exact : kind_rel;
         out[5 * k] = dist(best_out);
         out[5 * k + 1] = (float)kind;
         out[5 * k + 2] = (float)vars.size();

@@ -208,10 +208,11 @@ class Scene:
     def explain(self, view_inv, proj_inv, width, height, rays, target_rgb, tol=1e-4, max_pairs=4096, ncams=1,
                 threads=0, **kw):
         """Each ray re-marched with its flagged decisions taken the other way (oracle_scene_explain): the base march,
-        each single variant, then pairs of variants of two different decisions, until one is within tol plus its own
-        value bound (max |d rgb|; FLAG_VALUE_EPS in gvrt_oracle.cpp) of target_rgb (n x 3, e.g. the GPU's values).
-        Returns dict(dist, kind (0 base, 1 single flip, 2 pair), variants, decisions, vbound, alt_rgba): a ray is
-        explained when dist <= tol + vbound."""
+        each single variant, then pairs of variants of two different decisions, until one is within tol of target_rgb
+        (n x 3, e.g. the GPU's values; max |d rgb|); without such an exact alternative, the one closest to within tol
+        plus its own value bound (FLAG_VALUE_EPS in gvrt_oracle.cpp).  Returns dict(dist, kind (0 base, 1 single
+        flip, 2 pair), variants, decisions, vbound, alt_rgba): a ray is explained when dist <= tol + vbound, exactly
+        when dist <= tol."""
         p = default_params(proxy_mode=self.proxy_mode, **self.kw, **kw)
         vi = np.ascontiguousarray(view_inv, np.float32).reshape(-1)
         pi = np.ascontiguousarray(proj_inv, np.float32).reshape(16)
