@@ -26,11 +26,11 @@ def _scene(gv, name):
     return gv.scene.make(**gen), W, H, ncams
 
 
-def _oracle_subset(O, splats, vi, pi, W, H, ncams=1, stride=1):
-    """The oracle on every stride-th ray of the frame(s) (stride 1: all of them); the scene stays open for
-    explain_flagged (the caller closes it)."""
+def _oracle_subset(O, splats, vi, pi, W, H, ncams=1, stride=1, offset=0):
+    """The oracle on every stride-th ray of the frame(s) from `offset` (stride 1: all of them); the scene stays open
+    for explain_flagged (the caller closes it)."""
     e = O.enclose(splats)
-    sub = np.arange(0, W * H * ncams, stride, dtype=np.uint64)
+    sub = np.arange(offset, W * H * ncams, stride, dtype=np.uint64)
     sc = O.Scene(e)
     ref = sc.render(vi, pi, W, H, ncams=ncams, subset=None if stride == 1 else sub, margin=True)
     if stride == 1:
@@ -138,11 +138,13 @@ def test_lightfield_grid_16_views(gv, O):
 
 
 @pytest.mark.timeout(900)
-def test_dense_standin(gv, O):
+@pytest.mark.parametrize("half", [0, 1])
+def test_dense_standin(gv, O, half):
     """The dense stand-in (scene.dense_standin: ~150 crossings, ~79 accepted, ~10 LITERAL rounds per ray):
     FAST and LITERAL vs the oracle on every 2nd ray of the 1080p frame (1.04 M rays; the oracle's ~10 LITERAL
     rounds of ~150 crossings per ray make the whole frame take ~10 min on the GPU box's 16 threads, too long for
-    one test), FAST's accepted-hit counts vs the oracle's on every off-threshold ray."""
+    one test), in two tests of every 4th ray (offsets 0 and 2, ~85 s each), FAST's accepted-hit counts vs the
+    oracle's on every off-threshold ray."""
     splats, W, H, _ = _scene(gv, "dense")
     vi, pi = gv.scene.mipnerf_camera(W, H)
     with gv.Renderer(0) as r:
@@ -150,7 +152,7 @@ def test_dense_standin(gv, O):
         assert r.stats()["bvh_leaves"] > m
         fast = r.render(vi, pi, W, H, hit_counts=True)
         lit = r.render(vi, pi, W, H, mode=gv.MODE_LITERAL)
-    m_ref, sub, ref, sc = _oracle_subset(O, splats, vi, pi, W, H, stride=2)
+    m_ref, sub, ref, sc = _oracle_subset(O, splats, vi, pi, W, H, stride=4, offset=2 * half)
     assert m_ref == m
     st = ref["stats"].reshape(-1, 3)
     assert st[:, 0].mean() > 140, st.mean(axis=0)  # the workload is what it claims to be
@@ -167,7 +169,7 @@ def test_dense_standin(gv, O):
         ex_lit = explain_flagged(O, sc, vi, pi, W, H, lit["rgba32f"].reshape(-1, 4)[idx], ref, rays=sub)
     finally:
         sc.close()
-    record_parity("dense", stride=2, **parity_figures(O, gv, fast["rgba32f"].reshape(-1, 4)[idx], ref), **ex,
-                  literal=ex_lit)
+    record_parity("dense" if half == 0 else "dense_b", stride=4, offset=2 * half,
+                  **parity_figures(O, gv, fast["rgba32f"].reshape(-1, 4)[idx], ref), **ex, literal=ex_lit)
     assert_explained(ex)
     assert_explained(ex_lit)
