@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="bicycle",
-                    choices=["bicycle", "garden", "truck", "lightfield", "config1", "dense"])
+                    choices=["bicycle", "garden", "truck", "lightfield", "config1", "dense", "trained"])
     ap.add_argument("--split", default="auto", choices=["auto", "views", "tiles"],
                     help="auto: tiles for --config truck (config 4, strong scaling), else views")
     ap.add_argument("--mode", default="fast", choices=["fast", "literal"])
