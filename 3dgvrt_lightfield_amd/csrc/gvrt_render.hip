@@ -1336,7 +1336,9 @@ gvrt_status gvrt_launch_node_octants(gvrt_context* c) {
 // children are tested over [tlo - D, tc + D], D the largest of its leaves' (pad[2]; 0 elsewhere and in the
 // proxy-box nodes).  Nodes with inner children keep their proxy boxes: one D per node would widen the inner
 // children's range too (every node on E boxes refit upwards, or a per-child D, measured slower: DESIGN.md §4).
-// Which crossings are admitted does not change, only which leaves a wave visits.
+// Which crossings are admitted does not change, only which leaves a wave visits.  A split piece (SplitBLAS
+// analogue) admits only the crossings in its own box, so its acceptance box is E's box clipped to the piece's box
+// grown by the leaf's own D (the line's point in E lies within D of such a crossing); a piece E cannot reach is dropped.
 constexpr float ICO_CIRCUM = 1.2584086f;  // icosahedron circumradius / inradius
 __device__ inline bool slot_empty(const Bvh4Node& n, int k) { return n.box[k][0] > 1e37f; }
 __device__ inline void set_empty(Bvh4Node& n, int k) {
