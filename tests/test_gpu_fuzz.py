@@ -5,7 +5,8 @@ oracle alternative with its flagged decisions taken the other way (explain_flagg
 
 Each case draws: the scene family (config-1 cube, Mip-NeRF-like stand-in, dense stand-in, trained-splat stand-in) and
 its size, scale and opacity; the enclosing (default, or adaptive clamping with kernelMinResponse 0.0113 / 0.05,
-particlePrimitives.comp:81-105); an orbit camera (radius, elevation, azimuth, field of view) and a frame size; the
+particlePrimitives.comp:81-105); an orbit camera (radius, elevation, azimuth, field of view) or a light-field rig of
+up to 3 x 2 cameras in one launch, and a frame size; the
 kernel (FAST at 8 / 16 / 24 / 32 slots, LITERAL); the ray-generation variant (RQ corner rays, or the RT pipeline's
 pixel centres with alpha starting at 1, Q10 / Q11); the render thresholds (minTransmittance, hitMinGaussianResponse,
 alphaMinThreshold, SH degree; VulkanUtils.h:35-68); the build (device LBVH, the quality build with large-proxy
@@ -40,8 +41,17 @@ def _case(gv, seed):
         radius = float(rng.uniform(3.0, 6.0))
     W, H = int(rng.integers(96, 260)), int(rng.integers(64, 200))
     eye = gv.camera.orbit_eye(radius, float(rng.uniform(-30, 60)), float(rng.uniform(0, 360)))
-    vi, pi = gv.camera.pinhole(eye, (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), float(rng.uniform(25, 70)),
-                               gv.camera.aspect_ratio(W, H))
+    fovy = float(rng.uniform(25, 70))
+    ncams = 1
+    rig = np.random.default_rng(5000 + seed)  # (its own stream: the other draws of a seed stay as they were)
+    if rig.random() < 0.2:  # a light-field rig in one launch (multi-origin: per-camera record copies)
+        nx, ny = int(rig.integers(1, 4)), int(rig.integers(1, 3))
+        ncams = nx * ny
+        vi, pi = gv.camera.lightfield_grid_rig(eye, (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), nx=nx, ny=ny,
+                                                spacing=float(rig.uniform(0.05, 0.3)), fovy_deg=fovy,
+                                                aspect=gv.camera.aspect_ratio(W, H))
+    else:
+        vi, pi = gv.camera.pinhole(eye, (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), fovy, gv.camera.aspect_ratio(W, H))
     literal = rng.random() < 0.3
     depth = 0 if literal else int(rng.choice(DEPTHS))
     rt = rng.random() < 0.4
@@ -52,30 +62,30 @@ def _case(gv, seed):
                        alpha_min=float(rng.choice([1.0 / 255.0, 0.02])), sph_eval_degree=int(rng.integers(0, 4)))
     enc = dict(kernel_min_response=float(rng.choice([0.0113, 0.05])), opts=1) if rng.random() < 0.25 else {}
     build = [dict(), dict(gv.QUALITY_BUILD), dict(builder=2, collapse=1, split_cells=10)][int(rng.integers(3))]
-    return dict(kind=kind, splats=s, W=W, H=H, vi=vi, pi=pi, literal=literal, depth=depth, variant=variant,
-                build=build, enc=enc)
+    return dict(kind=kind, splats=s, W=W, H=H, vi=vi, pi=pi, ncams=ncams, literal=literal, depth=depth,
+                variant=variant, build=build, enc=enc)
 
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("seed", range(120))
 def test_random_case_vs_oracle(gv, O, seed):
     c = _case(gv, seed)
-    W, H, vi, pi = c["W"], c["H"], c["vi"], c["pi"]
+    W, H, vi, pi, nc = c["W"], c["H"], c["vi"], c["pi"], c["ncams"]
     mode = gv.MODE_LITERAL if c["literal"] else gv.MODE_FAST
     with gv.Renderer(0) as r:
         m = r.prepare(c["splats"], **c["build"], **c["enc"])
         kw = dict(c["variant"])
         if not c["literal"]:
             kw["kbuffer_depth"] = c["depth"]
-        out = r.render(vi, pi, W, H, mode=mode, hit_counts=True, **kw)
+        out = r.render(vi, pi, W, H, ncams=nc, mode=mode, hit_counts=True, **kw)
     e = O.enclose(c["splats"], **c["enc"])
     assert e["m"] == m
     sc = O.Scene(e, **c["enc"])
     try:
-        ref = sc.render(vi, pi, W, H, margin=True, **c["variant"])
-        ref = {k: v.reshape(W * H, -1) for k, v in ref.items()}
+        ref = sc.render(vi, pi, W, H, ncams=nc, margin=True, **c["variant"])
+        ref = {k: v.reshape(W * H * nc, -1) for k, v in ref.items()}
         got = out["rgba32f"].reshape(-1, 4)
-        desc = {k: c[k] for k in ("kind", "W", "H", "literal", "depth", "variant", "build", "enc")}
+        desc = {k: c[k] for k in ("kind", "W", "H", "ncams", "literal", "depth", "variant", "build", "enc")}
         print(f"case {seed}: {desc}, M {m}, flagged {O.ambiguous(ref['margin']).mean():.4f}")
         # the flags are the oracle's and depend only on the scene and camera; dense close-ups and small Gaussians
         # seen from afar (ill-conditioned values) flag the most: up to 18 % of a case's rays
@@ -83,7 +93,7 @@ def test_random_case_vs_oracle(gv, O, seed):
         if not c["literal"]:
             amb = O.ambiguous(ref["margin"])
             assert (out["hit_counts"].reshape(-1) != ref["stats"][:, 1])[~amb].sum() == 0
-        ex = explain_flagged(O, sc, vi, pi, W, H, got, ref, **c["variant"])
+        ex = explain_flagged(O, sc, vi, pi, W, H, got, ref, ncams=nc, **c["variant"])
         print(f"case {seed}: explained {ex['explained_by_single_flip']} single, {ex['explained_by_pair']} pair, "
               f"{ex['explained_by_value_bound_only']} value bound")
     finally:
